@@ -1,0 +1,127 @@
+/*
+ * bgx.h — C ABI of the MI355X-native backgammon self-play engine (libbgx.so).
+ *
+ * Plain C: pointers and sizes only, no exceptions, no torch/HIP types.  Every
+ * device pointer is a HIP device allocation on the engine's device; `stream`
+ * is a hipStream_t passed as void* (NULL = the default stream).  All work is
+ * enqueued on that stream; no entry point synchronises the host unless it says
+ * so.  Return value: BGX_OK (0) or a negative bgx_status.
+ *
+ * Each entry point names the reference interface it replaces
+ * (Nick-qsv/MLP-PPO-2PLY-P3, paths relative to its src/).
+ *
+ * Data formats
+ *   board52   int8[52]  = P1 points[24], P2 points[24], bar[2] (P1,P2), off[2]
+ *                         (the reference's (4,24) int8 tensor, immutable_board.py:20-24,
+ *                          with its 44 always-zero bytes dropped)
+ *   move      uint64    = up to 4 sub-moves, sub-move i in bits 16i..16i+15:
+ *                         start(5) | end(5)<<5 | hits_blot(1)<<10 | valid(1)<<15,
+ *                         start/end are Position values (0..23, BAR=24, BEAR_OFF=25)
+ *                         (SubMove/FullMove, moves/move_types.py:38-48)
+ *   features  float[198] per board (immutable_board.py:171-212)
+ *   info      int32 per lane: mover | (winner+1)<<8 | game_score<<16 | kind<<24,
+ *                         kind 0 = move, 1 = pass, 2 = invalid action, 3 = reset on game over
+ */
+#ifndef BGX_H
+#define BGX_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bgx_engine bgx_engine;
+
+enum bgx_status {
+    BGX_OK = 0,
+    BGX_EINVAL = -1,     /* bad argument */
+    BGX_EDEVICE = -2,    /* HIP error (launch, memory, device selection) */
+    BGX_ENOMEM = -3,     /* device allocation failed */
+    BGX_EOVERFLOW = -4   /* a position exceeded the slow-path dedup capacity */
+};
+
+enum bgx_dice_mode {
+    BGX_DICE_MT_LANE = 0,    /* lane i == one BackgammonEnv after env.seed(seeds[i]) (numpy legacy MT19937) */
+    BGX_DICE_MT_SHARED = 1,  /* one numpy stream consumed in lane order == VectorizedBackgammonEnv after np.random.seed */
+    BGX_DICE_PHILOX = 2      /* Philox4x32-10 per lane (speed mode; same die distribution) */
+};
+
+/* BackgammonEnv(match_length, max_legal_moves) x batch (backgammon_env.py:38-75,
+ * vec_bg_env.py:8-18).  auto_reset=1: a finished game is reset inside the same
+ * step and the post-reset observation is returned (VectorizedBackgammonEnv.step,
+ * vec_bg_env.py:35-36); auto_reset=0: BackgammonEnv semantics (the NEXT step
+ * resets and returns done=1, backgammon_env.py:119-121). */
+int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t seed, int32_t dice_mode,
+                      int32_t auto_reset, int32_t match_length, bgx_engine** out);
+int bgx_engine_destroy(bgx_engine* e);
+
+/* BackgammonEnv.seed (backgammon_env.py:357-363): per-lane MT19937 seeds
+ * (host array of `batch` uint32; mode SHARED uses seeds[0]); Philox: key = seed. */
+int bgx_engine_seed(bgx_engine* e, const uint32_t* seeds_host, uint64_t philox_seed);
+
+/* Device buffers owned by the engine (read-only for callers unless stated). */
+typedef struct {
+    uint8_t* lanes;      /* [batch][64] lane records: board52, cur(52), roll(53,54), game_over(55),
+                            match_over(56), score P1/P2 (57,58), n_moves int16 (60,61) */
+    uint64_t* moves;     /* [batch][max_moves] legal moves of the current position */
+    int32_t* n_total;    /* [batch] untruncated legal-move count (len before [:max_moves]) */
+    int32_t batch, max_moves;
+} bgx_buffers;
+int bgx_engine_buffers(bgx_engine* e, bgx_buffers* out);
+
+/* BackgammonEnv.reset (backgammon_env.py:78-113) for lanes with lane_mask[i]!=0
+ * (lane_mask NULL = all lanes).  obs_dev: float[batch][198] (all lanes written). */
+int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void* stream);
+
+/* BackgammonEnv.step / VectorizedBackgammonEnv.step (backgammon_env.py:115-191,
+ * vec_bg_env.py:28-49) on every lane.  actions_dev int32[batch]; outputs
+ * obs float[batch][198], reward float[batch], done uint8[batch], info int32[batch]
+ * (info_dev may be NULL). */
+int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* reward_dev, uint8_t* done_dev,
+             int32_t* info_dev, void* stream);
+
+/* get_all_possible_moves (moves/get_all_moves.py:9-70) + truncation to max_moves
+ * (backgammon_env.py:219-231) on n arbitrary positions.  boards52_dev int8[n][52],
+ * players_dev uint8[n], dice_dev uint8[n][2]; outputs n_moves int16[n] (truncated),
+ * n_total int32[n] (untruncated, may be NULL), moves uint64[n][max_moves]. */
+int bgx_movegen(bgx_engine* e, const int8_t* boards52_dev, const uint8_t* players_dev, const uint8_t* dice_dev,
+                int32_t n, int32_t max_moves, int16_t* n_moves_dev, int32_t* n_total_dev, uint64_t* moves_dev,
+                void* stream);
+
+/* ImmutableBoard.get_board_features (immutable_board.py:171-212) /
+ * get_board_features_batch_from_tensors (ai/batching.py:78-147). */
+int bgx_encode(const int8_t* boards52_dev, const uint8_t* players_dev, int32_t n, float* out_dev, void* stream);
+
+/* execute_full_move_on_board_copy (immutable_board.py:224-233) over every legal
+ * move of lanes [lane0, lane0+nlanes): boards52 int8[nlanes][max_moves][52]
+ * (rows past n_moves are zero). */
+int bgx_afterstates(bgx_engine* e, int32_t lane0, int32_t nlanes, int8_t* boards52_dev, void* stream);
+
+/* generate_all_board_features + zero padding (ai/batching.py:10-75,
+ * backgammon_env.py:207-243) for lanes [lane0, lane0+nlanes):
+ * out float[nlanes][max_moves][198], the mover's one-hot. */
+int bgx_legal_features(bgx_engine* e, int32_t lane0, int32_t nlanes, float* out_dev, void* stream);
+
+/* Copy lane state [lane0, lane0+n) out of the engine (device-to-device, async):
+ * lanes_dst uint8[n][64], moves_dst uint64[n][max_moves], n_total_dst int32[n];
+ * any destination may be NULL.  (The reference exposes env.board / env.legal_moves
+ * / env.current_player / env.roll_result as attributes, backgammon_env.py:51-75.) */
+int bgx_copy_lanes(bgx_engine* e, int32_t lane0, int32_t n, uint8_t* lanes_dst, uint64_t* moves_dst,
+                   int32_t* n_total_dst, void* stream);
+
+/* Overwrite lane records [lane0, lane0+n) (board52 + metadata, 64 bytes each) and
+ * re-enumerate their legal moves for the stored player/roll: lets a caller pose
+ * arbitrary positions (tests, analysis).  lanes_src uint8[n][64] on the device. */
+int bgx_set_lanes(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_src, void* stream);
+
+/* Sticky device error word (bit 0: a position overflowed the slow-path dedup
+ * table).  Synchronises the engine's device. */
+int bgx_engine_error(bgx_engine* e, int32_t* err_out);
+
+/* Last HIP error string of this thread (diagnostics). */
+const char* bgx_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BGX_H */

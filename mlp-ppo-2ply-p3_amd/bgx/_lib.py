@@ -1,0 +1,68 @@
+"""ctypes binding of libbgx.so (the C ABI in include/bgx.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950) and
+must be present: there is no CPU fallback for the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbgx.so")
+
+BGX_OK, BGX_EINVAL, BGX_EDEVICE, BGX_ENOMEM, BGX_EOVERFLOW = 0, -1, -2, -3, -4
+DICE_MT_LANE, DICE_MT_SHARED, DICE_PHILOX = 0, 1, 2
+
+# (name, restype, argtypes) for every symbol declared in include/bgx.h
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+SIGNATURES = {
+    "bgx_engine_create": (ctypes.c_int, [ctypes.c_int, _I32, _I32, ctypes.c_uint64, _I32, _I32, _I32,
+                                         ctypes.POINTER(_P)]),
+    "bgx_engine_destroy": (ctypes.c_int, [_P]),
+    "bgx_engine_seed": (ctypes.c_int, [_P, _P, ctypes.c_uint64]),
+    "bgx_engine_buffers": (ctypes.c_int, [_P, _P]),
+    "bgx_reset": (ctypes.c_int, [_P, _P, _P, _P]),
+    "bgx_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),
+    "bgx_movegen": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P]),
+    "bgx_encode": (ctypes.c_int, [_P, _P, _I32, _P, _P]),
+    "bgx_afterstates": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    "bgx_legal_features": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    "bgx_copy_lanes": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P]),
+    "bgx_set_lanes": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    "bgx_engine_error": (ctypes.c_int, [_P, _P]),
+    "bgx_last_error": (ctypes.c_char_p, []),
+}
+
+
+class BgxBuffers(ctypes.Structure):
+    _fields_ = [("lanes", _P), ("moves", _P), ("n_total", _P), ("batch", _I32), ("max_moves", _I32)]
+
+
+_lib = None
+
+
+class BgxError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libbgx.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BgxError(f"{LIB_PATH} missing: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != BGX_OK:
+        msg = load().bgx_last_error()
+        raise BgxError(f"{what} failed: status {rc} ({msg.decode() if msg else ''})")

@@ -1,0 +1,325 @@
+// bg_core.h — device-side backgammon rules for gfx950 (CDNA4).
+//
+// One WAVEFRONT owns one game.  The move tree is walked as a wave-uniform
+// (SGPR) program over bitboards: the mover's 24 point counts live in a 96-bit
+// nibble vector, and the opponent is reduced to two 24-bit masks (blocked =
+// opp>=2, blot = opp==1) because the opponent never moves during enumeration.
+// The dedup set of afterstates ("add_unique_board", handle_moves.py:313-341) is
+// an open-addressing table in LDS probed 64 slots at a time (one ds_read_b128
+// per lane + two ballots).
+//
+// Exactness: the afterstate of any sub-move sequence from a fixed root is
+// determined by (own counts, own bar, own off, set of hit blots); that 128-bit
+// KEY is a bijection of the reference's full (4,24) tensor given the root (opp
+// row = root opp - hits, opp bar = root bar + |hits|), so key equality ==
+// tensor-byte equality, the reference's dedup semantics (immutable_board.py:236).
+//
+// Citations are path:line in the reference's src/.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bg {
+
+constexpr int kBar = 24;   // moves/move_types.py:33
+constexpr int kOff = 25;   // moves/move_types.py:34
+constexpr uint32_t kHome[2] = {0xFC0000u, 0x3Fu};   // P1 home 18..23, P2 home 0..5 (conditions.py:122-126)
+
+// ------------------------------------------------------------------ state --
+struct Node {
+    uint64_t lo;      // own counts, points 0..15, 4 bits each
+    uint32_t hi;      // own counts, points 16..23
+    uint32_t k3;      // own_bar | own_off << 4 | hit-mask << 8
+    uint32_t occ;     // own > 0
+    uint32_t blot;    // opp == 1 and not hit yet
+    int n_home;       // own checkers on home points
+};
+
+__device__ __forceinline__ int own_at(const Node& s, int p) {
+    return p < 16 ? (int)((s.lo >> (4 * p)) & 15u) : (int)((s.hi >> (4 * (p - 16))) & 15u);
+}
+__device__ __forceinline__ void own_inc(Node& s, int p) {
+    if (p < 16) s.lo += 1ull << (4 * p); else s.hi += 1u << (4 * (p - 16));
+}
+__device__ __forceinline__ void own_dec(Node& s, int p) {
+    if (p < 16) s.lo -= 1ull << (4 * p); else s.hi -= 1u << (4 * (p - 16));
+}
+
+// A node's child list (get_moves_with_one_die, move_logic.py:20-44): bits 0..23
+// are normal-move sources in ascending order (move_logic.py:67); bit 31 is the
+// single special move (bar entry :95-137, or the one bear-off :211-253), which
+// always comes last.  Proof that at most one bear-off is ever emitted and that
+// it sorts after every normal move: DESIGN.md §"Move generation".
+struct Kids { uint32_t bits; int extra; };
+
+__device__ __forceinline__ int entry_point(int pl, int d) { return pl == 0 ? d - 1 : 24 - d; }
+
+__device__ __forceinline__ Kids gen(const Node& s, int d, int pl, uint32_t blocked) {
+    Kids k{0u, -1};
+    const int own_bar = (int)(s.k3 & 15u), own_off = (int)((s.k3 >> 4) & 15u);
+    if (own_off == 15) return k;                                   // GAME_OVER (:262-263)
+    if (own_bar > 0) {                                             // ON_BAR
+        const int dst = entry_point(pl, d);
+        if (!((blocked >> dst) & 1u)) { k.bits = 1u << 31; k.extra = kBar; }
+        return k;
+    }
+    const uint32_t home = kHome[pl];
+    uint32_t m;
+    if (pl == 0) m = s.occ & ~(blocked >> d) & ((1u << (24 - d)) - 1u);
+    else m = s.occ & ~(blocked << d) & 0xFFFFFFu & ~((1u << d) - 1u);
+    k.bits = m;
+    // BEAR_OFF: all_checkers_home (conditions.py:111-147); bar already 0 here.
+    if ((s.occ & ~home) == 0u && s.n_home + own_off == 15) {
+        if (pl == 0) {
+            const int far = __builtin_ctz(s.occ & home);          // :197-201
+            if (far + d >= 24) { k.extra = far; }
+            else { const int e = 24 - d; if (e != far && ((s.occ >> e) & 1u)) k.extra = e; }
+        } else {
+            const int far = 31 - __builtin_clz(s.occ & home);     // :203-208
+            if (far - d < 0) { k.extra = far; }
+            else { const int e = d - 1; if (e != far && ((s.occ >> e) & 1u)) k.extra = e; }
+        }
+        if (k.extra >= 0) k.bits |= 1u << 31;
+    }
+    return k;
+}
+
+struct Sub { int src, dst, hit; uint32_t enc; };
+
+// Child b of list k: (start, end, hits_blot) as SubMove (move_types.py:38-42),
+// encoded start | end<<5 | hit<<10 | valid<<15.
+__device__ __forceinline__ Sub child(const Node& s, const Kids& k, int b, int d, int pl) {
+    Sub m;
+    if (b == 31) { m.src = k.extra; m.dst = k.extra == kBar ? entry_point(pl, d) : kOff; }
+    else { m.src = b; m.dst = pl == 0 ? b + d : b - d; }
+    m.hit = m.dst < 24 ? (int)((s.blot >> m.dst) & 1u) : 0;
+    m.enc = (uint32_t)m.src | ((uint32_t)m.dst << 5) | ((uint32_t)m.hit << 10) | 0x8000u;
+    return m;
+}
+
+// move_checker (immutable_board.py:42-89) on the bitboard state; generated
+// sub-moves never take the reference's "invalid" branches.
+__device__ __forceinline__ Node apply(const Node& s, const Sub& m, int pl) {
+    Node t = s;
+    const uint32_t home = kHome[pl];
+    if (m.src == kBar) t.k3 -= 1u;
+    else {
+        own_dec(t, m.src);
+        if (own_at(t, m.src) == 0) t.occ &= ~(1u << m.src);
+        if ((home >> m.src) & 1u) t.n_home -= 1;
+    }
+    if (m.hit) { t.blot &= ~(1u << m.dst); t.k3 |= 1u << (8 + m.dst); }
+    if (m.dst == kOff) t.k3 += 16u;
+    else {
+        own_inc(t, m.dst);
+        t.occ |= 1u << m.dst;
+        if ((home >> m.dst) & 1u) t.n_home += 1;
+    }
+    return t;
+}
+
+// ----------------------------------------------------------- dedup tables --
+__device__ __forceinline__ uint32_t key_hash(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    uint32_t h = a * 0x9E3779B1u ^ (b * 0x85EBCA77u) ^ (c * 0xC2B2AE3Du) ^ (d * 0x27D4EB2Fu);
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    return h;
+}
+
+// Open addressing, linear probing, empty == all-zero key (a real afterstate
+// always has a non-zero own count/bar/off).  The whole wave probes 64
+// consecutive slots per step.  Never more than 7/8 full (callers enforce).
+template <int LOG_SLOTS, typename SlotPtr>
+__device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
+    const int lane = threadIdx.x & 63;
+    uint32_t base = key_hash(a, b, c, d);
+    for (;;) {
+        const uint32_t slot = (base + (uint32_t)lane) & mask;
+        const uint4 v = tab[slot];
+        const bool eq = v.x == a && v.y == b && v.z == c && v.w == d;
+        const bool em = (v.x | v.y | v.z | v.w) == 0u;
+        const uint64_t beq = __ballot(eq), bem = __ballot(em);
+        if (beq) return false;                 // no deletions: a match precedes any empty
+        if (bem) {
+            const int f = __ffsll((unsigned long long)bem) - 1;
+            if (lane == f) tab[slot] = make_uint4(a, b, c, d);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            return true;
+        }
+        base += 64u;
+    }
+}
+
+// ------------------------------------------------------------ enumeration --
+// Filtered-list bookkeeping (filter_full_moves_by_max_submoves,
+// get_all_moves.py:73-94): entries shorter than the running maximum can never
+// survive the final filter, so the kernel keeps only entries of the current
+// maximum length, in insertion order, and restarts the list when a longer one
+// appears.  The first `cap` survivors are written (env truncation,
+// backgammon_env.py:219-231); `count` keeps the untruncated total.
+template <int LOG_SLOTS, typename SlotPtr>
+struct Gen {
+    SlotPtr tab;
+    uint64_t* out;      // this game's move list, `cap` entries
+    int cap, pl;
+    uint32_t blocked;
+    int cur_max, count, n_unique, cap_unique;
+    bool ovf;
+
+    __device__ __forceinline__ void insert(const Node& s, uint64_t enc, int len) {
+        const uint32_t a = (uint32_t)s.lo, b = (uint32_t)(s.lo >> 32);
+        if (!table_insert<LOG_SLOTS>(tab, a, b, s.hi, s.k3)) return;
+        if (++n_unique >= cap_unique) { ovf = true; return; }
+        if (len > cur_max) { cur_max = len; count = 0; }
+        if (len == cur_max) {
+            if (count < cap && (threadIdx.x & 63) == 0) out[count] = enc;
+            ++count;
+        }
+    }
+
+    // handle_non_doubles (handle_moves.py:109-200)
+    __device__ __forceinline__ void pass_nd(const Node& s0, int da, int db) {
+        const Kids k1 = gen(s0, da, pl, blocked);
+        bool exists = false;
+        for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {          // pre-scan (:144-155)
+            const Sub m1 = child(s0, k1, __builtin_ctz(b1), da, pl);
+            const Node s1 = apply(s0, m1, pl);
+            if (gen(s1, db, pl, blocked).bits) { exists = true; break; }
+        }
+        for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
+            const Sub m1 = child(s0, k1, __builtin_ctz(b1), da, pl);
+            const Node s1 = apply(s0, m1, pl);
+            if (exists) {
+                const Kids k2 = gen(s1, db, pl, blocked);
+                for (uint32_t b2 = k2.bits; b2; b2 &= b2 - 1u) {
+                    const Sub m2 = child(s1, k2, __builtin_ctz(b2), db, pl);
+                    insert(apply(s1, m2, pl), (uint64_t)m1.enc | ((uint64_t)m2.enc << 16), 2);
+                    if (ovf) return;
+                }
+            } else {
+                insert(s1, (uint64_t)m1.enc, 1);
+                if (ovf) return;
+            }
+        }
+    }
+
+    // handle_doubles (handle_moves.py:203-310): 4-deep pre-order DFS; partial
+    // prefixes are inserted at dead ends only until the first 4-long sequence.
+    __device__ __forceinline__ void doubles(const Node& s0, int d) {
+        bool got4 = false;
+        const Kids k1 = gen(s0, d, pl, blocked);
+        for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
+            const Sub m1 = child(s0, k1, __builtin_ctz(b1), d, pl);
+            const Node s1 = apply(s0, m1, pl);
+            const Kids k2 = gen(s1, d, pl, blocked);
+            if (!k2.bits && !got4) { insert(s1, m1.enc, 1); if (ovf) return; }
+            for (uint32_t b2 = k2.bits; b2; b2 &= b2 - 1u) {
+                const Sub m2 = child(s1, k2, __builtin_ctz(b2), d, pl);
+                const Node s2 = apply(s1, m2, pl);
+                const uint64_t e2 = (uint64_t)m1.enc | ((uint64_t)m2.enc << 16);
+                const Kids k3 = gen(s2, d, pl, blocked);
+                if (!k3.bits && !got4) { insert(s2, e2, 2); if (ovf) return; }
+                for (uint32_t b3 = k3.bits; b3; b3 &= b3 - 1u) {
+                    const Sub m3 = child(s2, k3, __builtin_ctz(b3), d, pl);
+                    const Node s3 = apply(s2, m3, pl);
+                    const uint64_t e3 = e2 | ((uint64_t)m3.enc << 32);
+                    const Kids k4 = gen(s3, d, pl, blocked);
+                    if (!k4.bits && !got4) { insert(s3, e3, 3); if (ovf) return; }
+                    for (uint32_t b4 = k4.bits; b4; b4 &= b4 - 1u) {
+                        const Sub m4 = child(s3, k4, __builtin_ctz(b4), d, pl);
+                        insert(apply(s3, m4, pl), e3 | ((uint64_t)m4.enc << 48), 4);
+                        if (ovf) return;
+                        got4 = true;
+                    }
+                }
+            }
+        }
+    }
+
+    // get_all_possible_moves (get_all_moves.py:9-70)
+    __device__ __forceinline__ void run(const Node& s0, int r0, int r1) {
+        cur_max = 0; count = 0; n_unique = 0; ovf = false;
+        if (r0 != r1) {
+            const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
+            pass_nd(s0, hi, lo);
+            if (ovf) return;
+            if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi);   // :41-53
+        } else {
+            doubles(s0, r0);
+        }
+    }
+};
+
+// ------------------------------------------------------- board <-> state --
+// Lane l holds byte l of a 64-byte lane record (bytes 0..51 = the board in the
+// product layout p1[24] p2[24] bar[2] off[2]).  Returns the wave-uniform node
+// of player `pl` plus the opponent masks.
+__device__ __forceinline__ Node node_from_bytes(int bv, int pl, uint32_t& blocked) {
+    const int lane = threadIdx.x & 63;
+    const int p = lane < 24 ? lane : 0;
+    int own = __shfl(bv, pl * 24 + p);
+    int opp = __shfl(bv, (1 - pl) * 24 + p);
+    if (lane >= 24) { own = 0; opp = 0; }
+    Node s;
+    s.occ = (uint32_t)__ballot(own > 0);
+    blocked = (uint32_t)__ballot(opp >= 2);
+    s.blot = (uint32_t)__ballot(opp == 1);
+    uint32_t w = (uint32_t)(own & 15) << (4 * (lane & 7));
+    w |= __shfl_xor(w, 1); w |= __shfl_xor(w, 2); w |= __shfl_xor(w, 4);
+    s.lo = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(w, 0) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(w, 8) << 32);
+    s.hi = (uint32_t)__builtin_amdgcn_readlane(w, 16);
+    const uint32_t own_bar = (uint32_t)__builtin_amdgcn_readlane(bv, 48 + pl);
+    const uint32_t own_off = (uint32_t)__builtin_amdgcn_readlane(bv, 50 + pl);
+    s.k3 = (own_bar & 15u) | ((own_off & 15u) << 4);
+    int nh = 0;
+    if (pl == 0) { for (int q = 18; q < 24; ++q) nh += (int)((s.hi >> (4 * (q - 16))) & 15u); }
+    else { for (int q = 0; q < 6; ++q) nh += (int)((s.lo >> (4 * q)) & 15u); }
+    s.n_home = nh;
+    return s;
+}
+
+// Inverse: the new byte for lane l (< 52) after the mover `pl` went from the
+// root (bytes bv) to node s.  Bytes >= 52 are returned unchanged.
+__device__ __forceinline__ int bytes_from_node(int bv, const Node& s, int pl) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t hits = s.k3 >> 8;
+    int v = bv;
+    if (lane < 48) {
+        const int row = lane / 24, p = lane - 24 * row;
+        if (row == pl) v = own_at(s, p);
+        else v = bv - (int)((hits >> p) & 1u);
+    } else if (lane == 48 + pl) v = (int)(s.k3 & 15u);
+    else if (lane == 49 - pl) v = bv + __builtin_popcount(hits);
+    else if (lane == 50 + pl) v = (int)((s.k3 >> 4) & 15u);
+    return v;
+}
+
+// ----------------------------------------------------------------- encoder --
+// get_board_features (immutable_board.py:171-212) == get_board_features_batch_
+// from_tensors (ai/batching.py:78-147): 198 f32 per board.
+__constant__ static const float kOff15[16] = {
+    0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
+    6.0f / 15.0f, 7.0f / 15.0f, 8.0f / 15.0f, 9.0f / 15.0f, 10.0f / 15.0f, 11.0f / 15.0f,
+    12.0f / 15.0f, 13.0f / 15.0f, 14.0f / 15.0f, 15.0f / 15.0f};
+
+// Feature f (0..197) of the board whose byte l is in lane l's `bv`.
+__device__ __forceinline__ float feature_at(int bv, int f, int cur) {
+    const int p = f >= 98 ? 1 : 0;
+    const int g = f - 98 * p;
+    int idx;
+    if (f >= 196) idx = 0;
+    else if (g < 96) idx = p * 24 + (g >> 2);
+    else idx = (g == 96 ? 48 : 50) + p;
+    const int n = __shfl(bv, idx);
+    if (f >= 196) return (f == 196) == (cur == 0) ? 1.0f : 0.0f;
+    if (g < 96) {
+        const int u = g & 3;
+        if (u < 3) return n >= u + 1 ? 1.0f : 0.0f;
+        return n >= 3 ? (float)(n - 3) * 0.5f : 0.0f;
+    }
+    if (g == 96) return (float)n * 0.5f;
+    return kOff15[n & 15];
+}
+
+}  // namespace bg
