@@ -1,0 +1,233 @@
+"""bench.py — self-play env steps/sec on MI355X (BASELINE.json metric).
+
+Default workload (N=1 line): BASELINE config C3 — B=65,536 concurrent games per
+GPU, one PPO rollout step per iteration = policy forward (BackgammonPolicyNetwork
+198->128->{500 logits, 1 value}) + masked-softmax sampling + env.step on every
+lane + rollout record (int8 lane boards, action, log-prob, value, reward, done)
+copied to pinned host memory.  `value` = env steps/s summed over ranks.
+
+  python bench.py --gpus N --steps K --warmup W [--workload c3|c1|c4]
+
+Multi-GPU: one process per GPU (torchrun), independent game shards (weak
+scaling), no collective on the rollout path; barrier + max-over-ranks timing.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "mlp-ppo-2ply-p3_amd")]
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c3", choices=["c3", "c1"])
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def dist_init():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, ws, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, ws: int) -> float:
+    if ws == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, ws: int) -> float:
+    if ws == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def cpu_baseline(seconds: float):
+    """The oracle (C restatement of the reference env, oracle/bgoracle.c) stepping a
+    random legal policy on ONE host core for ~`seconds`: the reported CPU baseline."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O
+    O.build()
+    env = O.Env(seed=0)
+    env.reset()
+    rng = np.random.RandomState(0)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        for _ in range(200):
+            n = int(env.state()[1][3])
+            _, _, done, _ = env.step(rng.randint(n) if n else 0)
+            if done:
+                env.reset()
+            steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": steps / el, "unit": "env steps/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} random-policy BackgammonEnv.step calls of the C oracle (oracle/bgoracle.c), "
+                      f"1 thread, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank, ws, local = dist_init()
+    dev = torch.device("cuda", local)
+    import bgx
+    from bgx.policy import PolicyNet
+
+    B = args.batch
+    eng = bgx.Engine(batch=B, max_moves=500, seed=1234 + 7919 * rank, dice="philox", auto_reset=True, device=dev)
+    eng.reset(want_obs=True)
+    torch.manual_seed(0)
+    net = PolicyNet(hidden_size=128, action_size=500).to(dev)
+    net.pack()
+    ring = 8
+    pin = {
+        "boards": torch.empty(ring, B, 64, dtype=torch.uint8).pin_memory(),
+        "act": torch.empty(ring, B, dtype=torch.int32).pin_memory(),
+        "logp": torch.empty(ring, B, dtype=torch.float32).pin_memory(),
+        "value": torch.empty(ring, B, dtype=torch.float32).pin_memory(),
+        "reward": torch.empty(ring, B, dtype=torch.float32).pin_memory(),
+        "done": torch.empty(ring, B, dtype=torch.uint8).pin_memory(),
+    }
+    copy_stream = torch.cuda.Stream(dev)
+    counts = torch.empty(B, dtype=torch.int16, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(99 + rank)
+    ev_pairs = []
+    state = {"i": 0}
+
+    def step(timed: bool):
+        i = state["i"]
+        state["i"] += 1
+        if args.workload == "c1":
+            eng.n_moves(out=counts)
+            act = (torch.rand(B, device=dev, generator=gen) * counts.clamp(min=1).float()).to(torch.int32)
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            eng.step(act, want_obs=False, want_info=False)
+            if timed:
+                e1.record()
+                ev_pairs.append((e0, e1))
+            return
+        rec = net.rollout_inputs(eng)                       # int8 lane boards (no fp32 obs round trip)
+        act, logp, value = net.act(rec, seed=4242 + rank, step=i)   # fused HIP policy step
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _, rew, done, _ = eng.step(act, want_obs=False, want_info=False)
+        if timed:
+            e1.record()
+            ev_pairs.append((e0, e1))
+        # rollout record -> pinned host ring (side stream, overlapped)
+        slot = i % ring
+        cur = torch.cuda.current_stream(dev)
+        copy_stream.wait_stream(cur)
+        with torch.cuda.stream(copy_stream):
+            for k, v in (("boards", rec), ("act", act), ("logp", logp), ("value", value),
+                         ("reward", rew), ("done", done)):
+                pin[k][slot].copy_(v, non_blocking=True)
+                v.record_stream(copy_stream)
+        cur.wait_stream(copy_stream) if slot == ring - 1 else None
+
+    # warmup + a sample of legal-move counts for the algorithmic byte count
+    nm_sum, nm_n = 0.0, 0
+    for w in range(args.warmup):
+        step(False)
+        if w >= args.warmup // 2:
+            nm_sum += float(eng.n_moves(out=counts).float().mean().item())
+            nm_n += 1
+    mean_moves = nm_sum / max(nm_n, 1)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    torch.cuda.synchronize(dev)
+    el = max_over_ranks(time.perf_counter() - t0, ws)
+    total_steps = sum_over_ranks(float(B * args.steps), ws)
+    value = total_steps / el
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
+    # algorithmic bytes per lane-step of the env-step kernel:
+    # record in+out 128, action 4, chosen move 8, new move list 8*n, reward 4, done 1, rng ctr 8+8
+    bytes_per_lane = 128 + 4 + 8 + 8 * mean_moves + 4 + 1 + 16
+    achieved = B * bytes_per_lane / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_step_traffic.json")
+    if os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": "self-play env steps/sec (whole node) + 2-ply evals/sec at batch=65536",
+        "value": value,
+        "unit": "env steps/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8 boards / bf16 policy MLP",
+        "data": "synthetic self-play (Philox dice), random-init BackgammonPolicyNetwork weights",
+        "config": {"workload": ("C3: B=65536 games/GPU PPO rollout step (policy 198->128->{500,1} + masked "
+                                "sample + env.step)") if args.workload == "c3" else
+                   "C1-on-GPU: B=65536 games/GPU random legal policy env.step",
+                   "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
+                   "parallelism": f"dp{ws} (independent game shards)"},
+        "roofline": {"kernel": "k_step<0> (apply + dice + move enumeration + dedup, one wave per game)",
+                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel_ms": kern_ms, "bytes_per_lane_step": bytes_per_lane,
+                     "mean_legal_moves": mean_moves},
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

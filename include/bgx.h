@@ -70,13 +70,14 @@ typedef struct {
 int bgx_engine_buffers(bgx_engine* e, bgx_buffers* out);
 
 /* BackgammonEnv.reset (backgammon_env.py:78-113) for lanes with lane_mask[i]!=0
- * (lane_mask NULL = all lanes).  obs_dev: float[batch][198] (all lanes written). */
+ * (lane_mask NULL = all lanes).  obs_dev: float[batch][198] (all lanes written; may be NULL). */
 int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void* stream);
 
 /* BackgammonEnv.step / VectorizedBackgammonEnv.step (backgammon_env.py:115-191,
  * vec_bg_env.py:28-49) on every lane.  actions_dev int32[batch]; outputs
  * obs float[batch][198], reward float[batch], done uint8[batch], info int32[batch]
- * (info_dev may be NULL). */
+ * (obs_dev and info_dev may be NULL: a rollout that stores int8 boards skips the
+ * 792-byte fp32 observation). */
 int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* reward_dev, uint8_t* done_dev,
              int32_t* info_dev, void* stream);
 
@@ -102,6 +103,12 @@ int bgx_afterstates(bgx_engine* e, int32_t lane0, int32_t nlanes, int8_t* boards
  * out float[nlanes][max_moves][198], the mover's one-hot. */
 int bgx_legal_features(bgx_engine* e, int32_t lane0, int32_t nlanes, float* out_dev, void* stream);
 
+/* BackgammonEnv.action_mask / VectorizedBackgammonEnv.get_action_masks
+ * (backgammon_env.py:232-236, vec_bg_env.py:51-56): counts_dev int16[batch]
+ * (= number of legal actions, mask = iota < count; may be NULL) and/or
+ * masks_dev float[batch][max_moves] (1.0 for the first count entries; may be NULL). */
+int bgx_action_masks(bgx_engine* e, int16_t* counts_dev, float* masks_dev, void* stream);
+
 /* Copy lane state [lane0, lane0+n) out of the engine (device-to-device, async):
  * lanes_dst uint8[n][64], moves_dst uint64[n][max_moves], n_total_dst int32[n];
  * any destination may be NULL.  (The reference exposes env.board / env.legal_moves
@@ -117,6 +124,26 @@ int bgx_set_lanes(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_
 /* Sticky device error word (bit 0: a position overflowed the slow-path dedup
  * table).  Synchronises the engine's device. */
 int bgx_engine_error(bgx_engine* e, int32_t* err_out);
+
+/* ---- policy network (agent/policy_network.py:44-75) + select_action (ppo_agent.py:138-191) ----
+ * Weights are packed once per update into MFMA operand order (fp32):
+ * bgx_policy_packed_size(H, A) floats; H <= 128.  Inputs are torch nn.Linear
+ * layouts: W1 [H][198], b1 [H], Wa [A][H], ba [A], wv [H], bv [1]. */
+int bgx_policy_packed_size(int32_t hidden, int32_t n_actions);
+int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const float* ba, const float* wv, const float* bv,
+                    int32_t hidden, int32_t n_actions, float* packed_dev, void* stream);
+
+/* One fused pass per game lane: features from the 64-byte lane record
+ * (bgx_buffers.lanes layout), relu(W1 x + b1), logits = Wa h + ba, value = wv h + bv,
+ * masked = logits + log(mask + 1e-45) with mask = [a < legal count], then
+ * action ~ Categorical(softmax(masked)) (Gumbel-max on Philox(seed, step, row, a))
+ * or argmax if greedy (eval mode, ppo_agent.py:188-191).  act_out int32[n],
+ * logp_out float[n] (log softmax(masked)[action]), value_out float[n];
+ * logits_out float[n][32*ceil((A+1)/32)] (raw logits, value at column A) may be
+ * NULL, as may logp_out/value_out. */
+int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed_dev, int32_t hidden, int32_t n_actions,
+                   uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out, float* value_out,
+                   float* logits_out, void* stream);
 
 /* Last HIP error string of this thread (diagnostics). */
 const char* bgx_last_error(void);

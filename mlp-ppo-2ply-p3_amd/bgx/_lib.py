@@ -29,9 +29,14 @@ SIGNATURES = {
     "bgx_encode": (ctypes.c_int, [_P, _P, _I32, _P, _P]),
     "bgx_afterstates": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     "bgx_legal_features": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    "bgx_action_masks": (ctypes.c_int, [_P, _P, _P, _P]),
     "bgx_copy_lanes": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P]),
     "bgx_set_lanes": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     "bgx_engine_error": (ctypes.c_int, [_P, _P]),
+    "bgx_policy_packed_size": (ctypes.c_int, [_I32, _I32]),
+    "bgx_policy_pack": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P]),
+    "bgx_policy_act": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, ctypes.c_uint64, ctypes.c_uint32, _I32, _P, _P, _P,
+                                      _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
 }
 

@@ -86,22 +86,25 @@ class Engine:
               "bgx_engine_seed")
 
     # ----------------------------------------------------------------- env --
-    def reset(self, lane_mask: torch.Tensor | None = None) -> torch.Tensor:
+    def reset(self, lane_mask: torch.Tensor | None = None, want_obs: bool = True) -> torch.Tensor:
         m = None
         if lane_mask is not None:
             m = lane_mask.to(device=self.device, dtype=torch.uint8).contiguous()
-        check(self._lib.bgx_reset(self._h, _ptr(m), _ptr(self.obs), self._stream()), "bgx_reset")
+        check(self._lib.bgx_reset(self._h, _ptr(m), _ptr(self.obs) if want_obs else None, self._stream()),
+              "bgx_reset")
         return self.obs
 
-    def step(self, actions: torch.Tensor):
+    def step(self, actions: torch.Tensor, want_obs: bool = True, want_info: bool = True):
         """Advance every lane by one BackgammonEnv.step; returns (obs, reward, done, info)
-        views of engine-owned buffers (overwritten by the next step)."""
+        views of engine-owned buffers (overwritten by the next step).  want_obs=False
+        skips the fp32 observation write (rollouts that keep int8 boards)."""
         a = actions
         if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype == torch.int32
                 and a.is_contiguous()):
             a = torch.as_tensor(a).to(device=self.device, dtype=torch.int32).contiguous()
-        check(self._lib.bgx_step(self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
-                                 _ptr(self.info), self._stream()), "bgx_step")
+        check(self._lib.bgx_step(self._h, _ptr(a), _ptr(self.obs) if want_obs else None, _ptr(self.reward),
+                                 _ptr(self.done), _ptr(self.info) if want_info else None, self._stream()),
+              "bgx_step")
         return self.obs, self.reward, self.done, self.info
 
     # --------------------------------------------------------------- state --
@@ -115,13 +118,30 @@ class Engine:
               "bgx_copy_lanes")
         return rec, mv, nt
 
+    def records(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Lane records only (uint8[B,64]: board52, mover, roll, flags, legal count)."""
+        if out is None:
+            out = torch.empty(self.batch, 64, dtype=torch.uint8, device=self.device)
+        check(self._lib.bgx_copy_lanes(self._h, 0, self.batch, _ptr(out), None, None, self._stream()),
+              "bgx_copy_lanes")
+        return out
+
     def set_lanes(self, records: torch.Tensor, lane0: int = 0):
         r = records.to(device=self.device, dtype=torch.uint8).contiguous()
         check(self._lib.bgx_set_lanes(self._h, lane0, r.shape[0], _ptr(r), self._stream()), "bgx_set_lanes")
 
-    def n_moves(self) -> torch.Tensor:
-        rec, _, _ = self.lanes()
-        return rec[:, R_NM0].to(torch.int32) | (rec[:, R_NM1].to(torch.int32) << 8)
+    def n_moves(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Legal-action count per lane (int16[B]); mask = arange(max_moves) < count."""
+        if out is None:
+            out = torch.empty(self.batch, dtype=torch.int16, device=self.device)
+        check(self._lib.bgx_action_masks(self._h, _ptr(out), None, self._stream()), "bgx_action_masks")
+        return out
+
+    def action_masks(self) -> torch.Tensor:
+        """float[B, max_moves] (VectorizedBackgammonEnv.get_action_masks, vec_bg_env.py:51-56)."""
+        out = torch.empty(self.batch, self.max_moves, dtype=torch.float32, device=self.device)
+        check(self._lib.bgx_action_masks(self._h, None, _ptr(out), self._stream()), "bgx_action_masks")
+        return out
 
     def afterstates(self, lane0: int = 0, n: int | None = None) -> torch.Tensor:
         n = self.batch - lane0 if n is None else n

@@ -1,0 +1,118 @@
+"""BackgammonPolicyNetwork (agent/policy_network.py:6-75) and the rollout-side
+policy step (select_action, agent/ppo_agent.py:138-191) over engine lanes.
+
+The module keeps the reference's parameter names (fc1, action_head, value_head)
+so state_dicts load both ways.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import ctypes
+
+from . import _lib
+from ._lib import check
+from .engine import encode, _ptr
+
+# log(0 + 1e-45) in fp32: the reference masks with logits + log(mask + 1e-45)
+# (ppo_agent.py:166), i.e. -103.27893 for illegal actions, not -inf.
+MASK_LOG = float(torch.log(torch.tensor(1e-45, dtype=torch.float32)))
+
+
+class PolicyNet(nn.Module):
+    """198 -> H -> {action logits [A], value [1]} with ReLU (policy_network.py:44-75)."""
+
+    def __init__(self, input_size: int = 198, hidden_size: int = 128, action_size: int = 500):
+        super().__init__()
+        self.fc1 = nn.Linear(input_size, hidden_size)
+        self.action_head = nn.Linear(hidden_size, action_size)
+        self.value_head = nn.Linear(hidden_size, 1)
+
+    def forward(self, x):
+        x = F.relu(self.fc1(x))
+        return self.action_head(x), self.value_head(x).squeeze(-1)
+
+    # ---------------------------------------------------------- rollout --
+    @staticmethod
+    def rollout_inputs(eng) -> torch.Tensor:
+        """The lanes' 64-byte records (int8 board + mover + legal count): the
+        rollout stores these instead of fp32 observations."""
+        return eng.records()
+
+    # ---------------------------------------------------- HIP fast path --
+    @torch.no_grad()
+    def pack(self) -> torch.Tensor:
+        """Pack the weights into the MFMA operand layout of bgx_policy_act (call
+        after every optimizer step)."""
+        L = _lib.load()
+        H, A = self.fc1.out_features, self.action_head.out_features
+        n = L.bgx_policy_packed_size(H, A)
+        if n < 0:
+            raise ValueError(f"unsupported policy shape H={H} A={A}")
+        dev = self.fc1.weight.device
+        ps = [t.detach().float().contiguous() for t in (self.fc1.weight, self.fc1.bias, self.action_head.weight,
+                                                         self.action_head.bias, self.value_head.weight,
+                                                         self.value_head.bias)]
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        check(L.bgx_policy_pack(*[_ptr(t) for t in ps], H, A, _ptr(out), s), "bgx_policy_pack")
+        self._packed = out
+        return out
+
+    @torch.no_grad()
+    def act(self, records: torch.Tensor, seed: int = 0, step: int = 0, greedy: bool = False,
+            packed: torch.Tensor | None = None, want_logits: bool = False):
+        """select_action (ppo_agent.py:138-191) for every lane in ONE fused HIP
+        kernel (encode -> MLP on MFMA -> masked softmax -> sample).  Returns
+        (action int32[B], log_prob f32[B], value f32[B][, logits])."""
+        L = _lib.load()
+        packed = packed if packed is not None else getattr(self, "_packed", None)
+        if packed is None:
+            packed = self.pack()
+        H, A = self.fc1.out_features, self.action_head.out_features
+        r = records.contiguous()
+        n = r.shape[0]
+        dev = r.device
+        act = torch.empty(n, dtype=torch.int32, device=dev)
+        logp = torch.empty(n, dtype=torch.float32, device=dev)
+        val = torch.empty(n, dtype=torch.float32, device=dev)
+        logits = torch.empty(n, 32 * ((A + 32) // 32), dtype=torch.float32, device=dev) if want_logits else None
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        check(L.bgx_policy_act(_ptr(r), n, _ptr(packed), H, A, int(seed) & (2**64 - 1), int(step) & 0xFFFFFFFF,
+                               int(bool(greedy)), _ptr(act), _ptr(logp), _ptr(val), _ptr(logits), s),
+              "bgx_policy_act")
+        if want_logits:
+            return act, logp, val, logits
+        return act, logp, val
+
+    @torch.no_grad()
+    def act_torch(self, records: torch.Tensor, generator=None):
+        """Same step composed from torch ops on encoded features (a slower
+        reference composition used by tests)."""
+        B = records.shape[0]
+        boards = records[:, :52].contiguous()
+        cur = records[:, 52].contiguous()
+        counts = records[:, 60].to(torch.int32) | (records[:, 61].to(torch.int32) << 8)
+        x = encode(boards, cur)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits, value = self(x)
+        logits = logits.float()
+        A = logits.shape[1]
+        legal = torch.arange(A, device=logits.device)[None, :] < counts[:, None]
+        masked = torch.where(legal, logits, logits + MASK_LOG)
+        logp_all = torch.log_softmax(masked, dim=-1)
+        act = torch.multinomial(logp_all.exp(), 1, generator=generator).squeeze(1)
+        logp = logp_all.gather(1, act[:, None]).squeeze(1)
+        return act.to(torch.int32), logp, value.float()
+
+
+def masked_probs(logits: torch.Tensor, masks: torch.Tensor) -> torch.Tensor:
+    """softmax(logits + log(mask + 1e-45)) exactly as ppo_agent.py:166-167."""
+    return torch.softmax(logits + (masks + 1e-45).log(), dim=-1)
+
+
+__all__ = ["PolicyNet", "masked_probs", "MASK_LOG", "math"]

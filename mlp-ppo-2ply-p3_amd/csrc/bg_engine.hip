@@ -336,7 +336,7 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
     if (PHASE != 2) bv = apply_lane(bv, gi, (int)ufl((uint32_t)actions[gi]), A, reward, done, info);
     if (PHASE != 1) {
         bv = advance_lane(bv, gi, A, tab);
-        write_obs(bv, obs + (size_t)gi * 198);
+        if (obs) write_obs(bv, obs + (size_t)gi * 198);
     }
     store_rec(A, gi, bv);
 }
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(64) void k_reset(Args A, const uint8_t* lane_mask, 
     if (sel) bv = wr(bv, R_NEED, NEED_RESET);
     if (!mark_only) {
         bv = advance_lane(bv, gi, A, tab);
-        write_obs(bv, obs + (size_t)gi * 198);
+        if (obs) write_obs(bv, obs + (size_t)gi * 198);
     }
     store_rec(A, gi, bv);
 }
@@ -496,6 +496,15 @@ __global__ __launch_bounds__(64) void k_legal(Args A, int lane0, void* out) {
             }
         }
     }
+}
+
+__global__ void k_action_masks(Args A, int16_t* counts, float* masks) {
+    const int gi = blockIdx.x;
+    const uint8_t* r = A.lanes + (size_t)gi * 64;
+    const int n = (int)r[R_NM0] | ((int)r[R_NM1] << 8);
+    if (counts && threadIdx.x == 0) counts[gi] = (int16_t)n;
+    if (masks)
+        for (int m = threadIdx.x; m < A.max_moves; m += blockDim.x) masks[(size_t)gi * A.max_moves + m] = m < n ? 1.0f : 0.0f;
 }
 
 // Re-enumerate the legal moves of caller-posed lanes (bgx_set_lanes).
@@ -650,7 +659,7 @@ int bgx_engine_buffers(bgx_engine* e, bgx_buffers* out) {
 }
 
 int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void* stream) {
-    if (!e || !obs_dev) return BGX_EINVAL;
+    if (!e) return BGX_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
@@ -668,7 +677,7 @@ int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void*
 
 int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* reward_dev, uint8_t* done_dev,
              int32_t* info_dev, void* stream) {
-    if (!e || !actions_dev || !obs_dev || !reward_dev || !done_dev) return BGX_EINVAL;
+    if (!e || !actions_dev || !reward_dev || !done_dev) return BGX_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
@@ -722,6 +731,16 @@ int bgx_legal_features(bgx_engine* e, int32_t lane0, int32_t nlanes, float* out_
     if (nlanes == 0) return BGX_OK;
     CK(hipSetDevice(e->device));
     hipLaunchKernelGGL(k_legal<1>, dim3(nlanes), dim3(64), 0, (hipStream_t)stream, e->a, lane0, (void*)out_dev);
+    CKL();
+    return BGX_OK;
+}
+
+int bgx_action_masks(bgx_engine* e, int16_t* counts_dev, float* masks_dev, void* stream) {
+    if (!e) return BGX_EINVAL;
+    if (!counts_dev && !masks_dev) return BGX_OK;
+    CK(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_action_masks, dim3(e->a.B), dim3(masks_dev ? 256 : 64), 0, (hipStream_t)stream, e->a,
+                       counts_dev, masks_dev);
     CKL();
     return BGX_OK;
 }

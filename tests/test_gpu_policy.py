@@ -1,0 +1,107 @@
+"""Fused policy kernel (bgx_policy_act) vs the reference BackgammonPolicyNetwork
+(golden G5 logits/values) and torch fp32.  Tolerance: 1e-5 absolute on logits,
+values and log-probs (BASELINE.json: MLP value outputs within 1e-5 fp32)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def bgx():
+    import bgx as _bgx
+    return _bgx
+
+
+def _records(boards, players, counts=None):
+    n = len(boards)
+    r = np.zeros((n, 64), np.uint8)
+    r[:, :52] = np.asarray(boards, np.int8).view(np.uint8)
+    r[:, 52] = players
+    c = np.full(n, 500) if counts is None else np.asarray(counts)
+    r[:, 60] = c & 0xFF
+    r[:, 61] = c >> 8
+    return torch.from_numpy(r).cuda()
+
+
+def _net(mlp, H):
+    from bgx.policy import PolicyNet
+    net = PolicyNet(hidden_size=H).cuda()
+    sd = {k[len(f"h{H}_"):]: torch.from_numpy(v) for k, v in mlp.items()
+          if k.startswith(f"h{H}_") and not k.endswith(("logits", "values"))}
+    net.load_state_dict(sd)
+    return net
+
+
+@pytest.mark.parametrize("H", [128, 40])
+def test_policy_logits_values_match_reference(bgx, golden, H):
+    mlp, feat, mg = golden("mlp"), golden("features"), golden("movegen")
+    idx = feat["obs_idx"][:600]
+    rec = _records(mg["boards"][idx], feat["obs_player"][:600])
+    net = _net(mlp, H)
+    act, logp, val, logits = net.act(rec, seed=1, step=0, want_logits=True)
+    lg = logits[:, :500].cpu().numpy()
+    assert np.abs(lg - mlp[f"h{H}_logits"][:600]).max() < TOL
+    assert np.abs(val.cpu().numpy() - mlp[f"h{H}_values"][:600]).max() < TOL
+    assert np.abs(logits[:, 500].cpu().numpy() - mlp[f"h{H}_values"][:600]).max() < TOL
+
+
+def test_policy_logp_and_greedy(bgx):
+    from bgx.policy import PolicyNet, masked_probs
+    torch.manual_seed(0)
+    net = PolicyNet(hidden_size=128).cuda()
+    eng = bgx.Engine(batch=4096, dice="philox", seed=5)
+    eng.reset()
+    for i in range(30):
+        rec = eng.records()
+        a, _, _ = net.act(rec, seed=3, step=i)
+        eng.step(a)
+    rec = eng.records()
+    counts = (rec[:, 60].int() | (rec[:, 61].int() << 8))
+    x = bgx.encode(rec[:, :52].contiguous(), rec[:, 52].contiguous())
+    with torch.no_grad():
+        lg, v = net(x)
+    masks = (torch.arange(500, device="cuda")[None] < counts[:, None]).float()
+    probs = masked_probs(lg, masks)
+    a, logp, val = net.act(rec, seed=7, step=1)
+    # zero legal moves: the reference softmaxes all 500 masked logits, any action passes
+    assert torch.all((a < counts) | (counts == 0))
+    legal = counts > 0
+    ref_logp = torch.log(probs.gather(1, a.long()[:, None]).squeeze(1))
+    assert (logp - ref_logp)[legal].abs().max().item() < 1e-4   # probs path goes through exp/log in fp32
+    lsm = torch.log_softmax(lg + (masks + 1e-45).log(), -1).gather(1, a.long()[:, None]).squeeze(1)
+    assert (logp - lsm).abs().max().item() < TOL
+    assert (val - v).abs().max().item() < TOL
+    g, _, _ = net.act(rec, greedy=True)
+    assert torch.equal(g.long(), torch.argmax(probs, -1))
+
+
+def test_policy_sampling_distribution(bgx):
+    """Empirical action frequencies of one position vs softmax(masked) (chi-square)."""
+    from bgx.policy import PolicyNet, masked_probs
+    torch.manual_seed(1)
+    net = PolicyNet(hidden_size=128).cuda()
+    with torch.no_grad():
+        net.action_head.weight.mul_(8.0)      # a peaked, non-uniform distribution
+    eng = bgx.Engine(batch=64, dice="philox", seed=11)
+    eng.reset()
+    rec = eng.records()
+    counts = (rec[:, 60].int() | (rec[:, 61].int() << 8)).cpu().numpy()
+    lane = int(np.argmax(counts))
+    n = int(counts[lane])
+    N = 200_000
+    reps = rec[lane:lane + 1].repeat(N, 1)
+    a, _, _ = net.act(reps, seed=123, step=9)
+    freq = np.bincount(a.cpu().numpy(), minlength=500)[:500] / N
+    x = bgx.encode(rec[lane:lane + 1, :52].contiguous(), rec[lane:lane + 1, 52].contiguous())
+    with torch.no_grad():
+        lg, _ = net(x)
+    mask = (torch.arange(500, device="cuda") < n).float()[None]
+    p = masked_probs(lg, mask)[0].cpu().numpy()
+    assert freq[n:].sum() == 0
+    keep = p[:n] * N > 20
+    chi2 = ((freq[:n][keep] - p[:n][keep]) ** 2 / p[:n][keep]).sum() * N
+    dof = int(keep.sum()) - 1
+    assert chi2 < dof + 6 * np.sqrt(2 * dof) + 10, (chi2, dof)
