@@ -59,6 +59,13 @@ int bgx_engine_destroy(bgx_engine* e);
  * (host array of `batch` uint32; mode SHARED uses seeds[0]); Philox: key = seed. */
 int bgx_engine_seed(bgx_engine* e, const uint32_t* seeds_host, uint64_t philox_seed);
 
+/* Read (set=0) or overwrite (set=1) the MT19937 state of one lane (mode
+ * MT_LANE) or of the shared stream (mode MT_SHARED, lane ignored):
+ * state_host uint32[625] = numpy's get_state() key[624] + pos.  Lets the
+ * drop-in classes draw dice from numpy's global RandomState exactly as the
+ * reference does (backgammon_env.py:245-246).  Synchronous. */
+int bgx_engine_mt_state(bgx_engine* e, int32_t lane, uint32_t* state_host, int32_t set);
+
 /* Device buffers owned by the engine (read-only for callers unless stated). */
 typedef struct {
     uint8_t* lanes;      /* [batch][64] lane records: board52, cur(52), roll(53,54), game_over(55),

@@ -22,6 +22,7 @@ SIGNATURES = {
                                          ctypes.POINTER(_P)]),
     "bgx_engine_destroy": (ctypes.c_int, [_P]),
     "bgx_engine_seed": (ctypes.c_int, [_P, _P, ctypes.c_uint64]),
+    "bgx_engine_mt_state": (ctypes.c_int, [_P, _I32, _P, _I32]),
     "bgx_engine_buffers": (ctypes.c_int, [_P, _P]),
     "bgx_reset": (ctypes.c_int, [_P, _P, _P, _P]),
     "bgx_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P]),

@@ -85,6 +85,15 @@ class Engine:
         check(self._lib.bgx_engine_seed(self._h, arr.ctypes.data_as(ctypes.c_void_p), int(philox_seed)),
               "bgx_engine_seed")
 
+    def mt_state(self, lane: int = 0, state=None):
+        """Get (state=None) or set the MT19937 state (uint32[625] = key + pos) of a
+        lane / of the shared stream: numpy RandomState.get_state() compatible."""
+        import numpy as np
+        buf = np.zeros(625, dtype=np.uint32) if state is None else np.ascontiguousarray(state, dtype=np.uint32)
+        check(self._lib.bgx_engine_mt_state(self._h, int(lane), buf.ctypes.data_as(ctypes.c_void_p),
+                                            0 if state is None else 1), "bgx_engine_mt_state")
+        return buf
+
     # ----------------------------------------------------------------- env --
     def reset(self, lane_mask: torch.Tensor | None = None, want_obs: bool = True) -> torch.Tensor:
         m = None
@@ -117,6 +126,13 @@ class Engine:
         check(self._lib.bgx_copy_lanes(self._h, lane0, n, _ptr(rec), _ptr(mv), _ptr(nt), self._stream()),
               "bgx_copy_lanes")
         return rec, mv, nt
+
+    def record(self, lane: int):
+        """One lane's 64-byte record as a host numpy array (synchronises)."""
+        r = torch.empty(1, 64, dtype=torch.uint8, device=self.device)
+        check(self._lib.bgx_copy_lanes(self._h, int(lane), 1, _ptr(r), None, None, self._stream()),
+              "bgx_copy_lanes")
+        return r.cpu().numpy()[0]
 
     def records(self, out: torch.Tensor | None = None) -> torch.Tensor:
         """Lane records only (uint8[B,64]: board52, mover, roll, flags, legal count)."""

@@ -651,6 +651,20 @@ int bgx_engine_seed(bgx_engine* e, const uint32_t* seeds_host, uint64_t philox_s
     return BGX_OK;
 }
 
+int bgx_engine_mt_state(bgx_engine* e, int32_t lane, uint32_t* state_host, int32_t set) {
+    if (!e || !state_host) return BGX_EINVAL;
+    Args& A = e->a;
+    if (A.dice_mode == BGX_DICE_PHILOX) return BGX_EINVAL;
+    if (A.dice_mode == BGX_DICE_MT_SHARED) lane = 0;
+    if (lane < 0 || lane >= A.B) return BGX_EINVAL;
+    CK(hipSetDevice(e->device));
+    CK(hipDeviceSynchronize());
+    uint32_t* dev = A.mt + (size_t)lane * kMtWords;
+    if (set) CK(hipMemcpy(dev, state_host, 625 * 4, hipMemcpyHostToDevice));
+    else CK(hipMemcpy(state_host, dev, 625 * 4, hipMemcpyDeviceToHost));
+    return BGX_OK;
+}
+
 int bgx_engine_buffers(bgx_engine* e, bgx_buffers* out) {
     if (!e || !out) return BGX_EINVAL;
     out->lanes = e->a.lanes; out->moves = e->a.moves; out->n_total = e->a.n_total;

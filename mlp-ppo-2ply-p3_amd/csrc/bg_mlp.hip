@@ -49,7 +49,7 @@ __device__ __forceinline__ float feat(const uint8_t* rec, int k) {
 
 __device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
 
-// Philox4x32-10 -> 4 uniforms in (0,1)
+// Philox4x32-10 -> 4 uniforms strictly inside (0,1)
 __device__ __forceinline__ void philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
                                         uint32_t k1, float u[4]) {
     #pragma unroll
@@ -61,7 +61,8 @@ __device__ __forceinline__ void philox4(uint32_t c0, uint32_t c1, uint32_t c2, u
     }
     const uint32_t w[4] = {c0, c1, c2, c3};
     #pragma unroll
-    for (int i = 0; i < 4; ++i) u[i] = ((float)(w[i] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    // 23 bits + 1/2: exactly representable, u in [2^-24, 1 - 2^-24] (never 0 or 1)
+    for (int i = 0; i < 4; ++i) u[i] = ((float)(w[i] >> 9) + 0.5f) * (1.0f / 8388608.0f);
 }
 
 // Packed weights (bgx_policy_pack):
@@ -151,7 +152,8 @@ __global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ r
                 const float mn = fmaxf(m, z);
                 s = s * __expf(m - mn) + __expf(z - mn);
                 m = mn;
-                const float key = greedy ? z : z - __logf(-__logf(u[r]));
+                // Gumbel(0,1) noise; accurate logf near u = 1
+                const float key = greedy ? z : z - logf(-logf(u[r]));
                 if (key > best) { best = key; besta = a; bestz = z; }
             }
         }

@@ -1,0 +1,80 @@
+"""The reference-API drop-in classes (bgx.BackgammonEnv, VectorizedBackgammonEnv,
+get_all_possible_moves, ImmutableBoard, ...) against the reference's golden
+traces: same calls, same numpy seeding, same results."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def bgx():
+    import bgx as _bgx
+    return _bgx
+
+
+def test_backgammon_env_trace(bgx, golden):
+    g = golden("traces")
+    for gi in [0, 1, 2, 3, 5, 7]:
+        sel = np.where(g["game"] == gi)[0]
+        env = bgx.BackgammonEnv(match_length=15 if gi % 5 else 3)
+        env.seed(gi)
+        obs = env.reset()
+        assert np.array_equal(obs.numpy(), g["first_obs"][gi])
+        for j in sel:
+            assert env.roll_result == [int(g["r0"][j]), int(g["r1"][j])]
+            assert int(env.action_mask.sum()) == g["n_legal"][j]
+            assert int(env.current_player) == g["mover"][j]
+            obs, rew, done, info = env.step(int(g["action"][j]))
+            assert float(rew) == g["reward"][j] and done == bool(g["done"][j])
+            assert int(info.get("winner", -1)) == g["winner"][j]
+            assert np.array_equal(bgx.types.tensor_to52(env.board.tensor).numpy(), g["board_after"][j])
+
+
+def test_vectorized_env_trace(bgx, golden):
+    g = golden("traces")
+    n_env = g["vec_obs0"].shape[0]
+    np.random.seed(777)
+    torch.manual_seed(777)
+    venv = bgx.VectorizedBackgammonEnv(num_envs=n_env)
+    obs = venv.reset()
+    assert np.array_equal(obs.numpy(), g["vec_obs0"])
+    for t in range(g["vec_actions"].shape[0]):
+        assert np.array_equal(venv.get_action_masks().sum(1).numpy().astype(int), g["vec_n_legal"][t])
+        obs, rew, done, infos = venv.step(g["vec_actions"][t])
+        assert np.array_equal(obs.numpy(), g["vec_obs"][t])
+        assert np.array_equal(rew.numpy(), g["vec_rewards"][t])
+        assert np.array_equal(done.numpy(), g["vec_dones"][t])
+    # numpy's global stream advanced exactly as the reference's did
+    assert len(infos) == n_env
+
+
+def test_get_all_possible_moves_api(bgx, golden):
+    g = golden("movegen")
+    offs = g["offsets"]
+    for i in list(range(0, len(g["counts"]), 37)) + [len(g["counts"]) - 1]:
+        board = bgx.ImmutableBoard(bgx.types.tensor_from52(torch.from_numpy(g["boards"][i])))
+        mv = bgx.get_all_possible_moves(bgx.Player(int(g["players"][i])), board, [int(x) for x in g["rolls"][i]])
+        enc = np.array([bgx.types.encode_move(m) for m in mv], np.uint64)
+        assert len(mv) == g["counts"][i]
+        assert np.array_equal(enc, g["moves"][offs[i]:offs[i + 1]])
+
+
+def test_legal_board_features_and_features(bgx, golden):
+    f, mg = golden("features"), golden("movegen")
+    row = 0
+    for pos, ln in list(zip(f["aft_pos"], f["aft_lens"]))[:40]:
+        board = bgx.ImmutableBoard(bgx.types.tensor_from52(torch.from_numpy(mg["boards"][pos])))
+        p = bgx.Player(int(mg["players"][pos]))
+        mv = bgx.get_all_possible_moves(p, board, [int(x) for x in mg["rolls"][pos]])
+        feats = bgx.generate_all_board_features(board, p, mv)
+        assert np.array_equal(feats.numpy(), f["aft"][row:row + ln])
+        row += ln
+    env = bgx.BackgammonEnv()
+    env.seed(3)
+    env.reset()
+    lbf = env.legal_board_features
+    n = int(env.action_mask.sum())
+    ref = bgx.generate_all_board_features(env.board, env.current_player, env.legal_moves)
+    assert lbf.shape == (500, 198) and torch.equal(lbf[:n], ref) and not lbf[n:].any()

@@ -100,8 +100,10 @@ def test_policy_sampling_distribution(bgx):
         lg, _ = net(x)
     mask = (torch.arange(500, device="cuda") < n).float()[None]
     p = masked_probs(lg, mask)[0].cpu().numpy()
-    assert freq[n:].sum() == 0
-    keep = p[:n] * N > 20
-    chi2 = ((freq[:n][keep] - p[:n][keep]) ** 2 / p[:n][keep]).sum() * N
+    # illegal actions keep the reference's tiny mass exp(z - 103.28) (not -inf)
+    pill = p[n:].sum()
+    assert abs(freq[n:].sum() - pill) <= 6 * np.sqrt(pill / N) + 1e-5
+    keep = p * N > 20
+    chi2 = ((freq[keep] - p[keep]) ** 2 / p[keep]).sum() * N
     dof = int(keep.sum()) - 1
     assert chi2 < dof + 6 * np.sqrt(2 * dof) + 10, (chi2, dof)
