@@ -35,6 +35,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=["c3", "c1"])
     ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--burn-in", type=int, default=150,
+                    help="untimed steps before warmup so the game population reaches its steady mix "
+                         "(openings are cheaper than mid-game positions)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
@@ -164,6 +167,8 @@ def main():
                 v.record_stream(copy_stream)
         cur.wait_stream(copy_stream) if slot == ring - 1 else None
 
+    for _ in range(args.burn_in):
+        step(False)
     # warmup + a sample of legal-move counts for the algorithmic byte count
     nm_sum, nm_n = 0.0, 0
     for w in range(args.warmup):
@@ -209,6 +214,7 @@ def main():
         "vs_baseline": None,
         "dtype": "int8 boards / bf16 policy MLP",
         "data": "synthetic self-play (Philox dice), random-init BackgammonPolicyNetwork weights",
+        "burn_in": args.burn_in,
         "config": {"workload": ("C3: B=65536 games/GPU PPO rollout step (policy 198->128->{500,1} + masked "
                                 "sample + env.step)") if args.workload == "c3" else
                    "C1-on-GPU: B=65536 games/GPU random legal policy env.step",

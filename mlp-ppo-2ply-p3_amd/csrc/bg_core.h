@@ -35,14 +35,20 @@ struct Node {
     int n_home;       // own checkers on home points
 };
 
+// branch-free (s_cselect) nibble access: point p lives in lo for p < 16, else hi
 __device__ __forceinline__ int own_at(const Node& s, int p) {
-    return p < 16 ? (int)((s.lo >> (4 * p)) & 15u) : (int)((s.hi >> (4 * (p - 16))) & 15u);
+    const uint64_t w = p < 16 ? s.lo : (uint64_t)s.hi;
+    return (int)((w >> (4 * (p & 15))) & 15u);
 }
 __device__ __forceinline__ void own_inc(Node& s, int p) {
-    if (p < 16) s.lo += 1ull << (4 * p); else s.hi += 1u << (4 * (p - 16));
+    const uint64_t m = 1ull << (4 * (p & 15));
+    s.lo += p < 16 ? m : 0ull;
+    s.hi += p < 16 ? 0u : (uint32_t)m;
 }
 __device__ __forceinline__ void own_dec(Node& s, int p) {
-    if (p < 16) s.lo -= 1ull << (4 * p); else s.hi -= 1u << (4 * (p - 16));
+    const uint64_t m = 1ull << (4 * (p & 15));
+    s.lo -= p < 16 ? m : 0ull;
+    s.hi -= p < 16 ? 0u : (uint32_t)m;
 }
 
 // A node's child list (get_moves_with_one_die, move_logic.py:20-44): bits 0..23
@@ -129,7 +135,8 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t a, uint32_t b, uint32_t c,
 // always has a non-zero own count/bar/off).  The whole wave probes 64
 // consecutive slots per step.  Never more than 7/8 full (callers enforce).
 template <int LOG_SLOTS, typename SlotPtr>
-__device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+__device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                             bool may_insert = true) {
     constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
     const int lane = threadIdx.x & 63;
     uint32_t base = key_hash(a, b, c, d);
@@ -142,7 +149,7 @@ __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b
         if (beq) return false;                 // no deletions: a match precedes any empty
         if (bem) {
             const int f = __ffsll((unsigned long long)bem) - 1;
-            if (lane == f) tab[slot] = make_uint4(a, b, c, d);
+            if (may_insert && lane == f) tab[slot] = make_uint4(a, b, c, d);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             return true;
         }
@@ -157,9 +164,23 @@ __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b
 // maximum length, in insertion order, and restarts the list when a longer one
 // appears.  The first `cap` survivors are written (env truncation,
 // backgammon_env.py:219-231); `count` keeps the untruncated total.
+// Revisit pruning for doubles (exact): the insert attempts of a subtree depend
+// only on its root state S and depth (plus got4, which only ever turns on).
+// When S is reached again at the same depth, every attempt it would make was
+// already made by the first visit (a partial prefix is attempted only while
+// got4 is off, and got4 off now means it was off throughout the first visit;
+// 4-long leaves are attempted unconditionally), so all of them are duplicates
+// and the revisit is a no-op: skip it.  Memo tables are per depth (2 and 3),
+// 256 slots each in LDS; when one fills up it stops recording (still exact).
+constexpr int kLogMemo = 8;
+constexpr int kMemoCap = (7 << kLogMemo) / 8;
+
 template <int LOG_SLOTS, typename SlotPtr>
 struct Gen {
     SlotPtr tab;
+    uint4* memo2;       // LDS memo tables (nullptr = no pruning)
+    uint4* memo3;
+    int n_memo2, n_memo3;
     uint64_t* out;      // this game's move list, `cap` entries
     int cap, pl;
     uint32_t blocked;
@@ -203,6 +224,15 @@ struct Gen {
         }
     }
 
+    // true if (s, depth) was seen before (=> skip); records it otherwise
+    __device__ __forceinline__ bool seen(const Node& s, uint4* memo, int& nm) {
+        if (!memo) return false;
+        const bool fresh = table_insert<kLogMemo>(memo, (uint32_t)s.lo, (uint32_t)(s.lo >> 32), s.hi, s.k3,
+                                                  nm < kMemoCap);
+        if (fresh && nm < kMemoCap) ++nm;
+        return !fresh;
+    }
+
     // handle_doubles (handle_moves.py:203-310): 4-deep pre-order DFS; partial
     // prefixes are inserted at dead ends only until the first 4-long sequence.
     __device__ __forceinline__ void doubles(const Node& s0, int d) {
@@ -216,12 +246,14 @@ struct Gen {
             for (uint32_t b2 = k2.bits; b2; b2 &= b2 - 1u) {
                 const Sub m2 = child(s1, k2, __builtin_ctz(b2), d, pl);
                 const Node s2 = apply(s1, m2, pl);
+                if (seen(s2, memo2, n_memo2)) continue;
                 const uint64_t e2 = (uint64_t)m1.enc | ((uint64_t)m2.enc << 16);
                 const Kids k3 = gen(s2, d, pl, blocked);
                 if (!k3.bits && !got4) { insert(s2, e2, 2); if (ovf) return; }
                 for (uint32_t b3 = k3.bits; b3; b3 &= b3 - 1u) {
                     const Sub m3 = child(s2, k3, __builtin_ctz(b3), d, pl);
                     const Node s3 = apply(s2, m3, pl);
+                    if (seen(s3, memo3, n_memo3)) continue;
                     const uint64_t e3 = e2 | ((uint64_t)m3.enc << 32);
                     const Kids k4 = gen(s3, d, pl, blocked);
                     if (!k4.bits && !got4) { insert(s3, e3, 3); if (ovf) return; }
@@ -238,7 +270,7 @@ struct Gen {
 
     // get_all_possible_moves (get_all_moves.py:9-70)
     __device__ __forceinline__ void run(const Node& s0, int r0, int r1) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
         if (r0 != r1) {
             const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
             pass_nd(s0, hi, lo);

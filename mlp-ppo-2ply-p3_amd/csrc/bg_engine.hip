@@ -25,8 +25,9 @@ using namespace bg;
 
 namespace {
 
-constexpr int kLogSlots = 10;                 // 1024-slot LDS dedup table (16 KiB)
-constexpr int kCapFast = (7 << kLogSlots) / 8;
+// LDS dedup table: 2^LOG slots x 16 B (LOG 9 = 8 KiB, 10 = 16 KiB); chosen at
+// engine creation (env BGX_LDS_LOG), capacity 7/8 of the slots.
+template <int LOG> constexpr int cap_fast() { return (7 << LOG) / 8; }
 constexpr int kLogSlotsSlow = 17;             // 131072-slot global table (2 MiB) per slow wave
 constexpr int kCapSlow = (7 << kLogSlotsSlow) / 8;
 constexpr int kSlowWaves = 32;
@@ -181,12 +182,17 @@ struct Args {
 // Returns n_moves (truncated); *total = untruncated count; *ovf on overflow.
 template <int LOG, typename SlotPtr>
 __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint64_t* out, int cap, SlotPtr tab,
-                                           int cap_unique, int* total, bool* ovf) {
+                                           int cap_unique, int* total, bool* ovf, uint4* memo) {
     constexpr int slots = 1 << LOG;
     for (int i = lane_id(); i < slots; i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
+    const bool dbl = r0 == r1;
+    if (memo && dbl)
+        for (int i = lane_id(); i < (2 << kLogMemo); i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     Gen<LOG, SlotPtr> g;
     g.tab = tab; g.out = out; g.cap = cap; g.pl = pl; g.cap_unique = cap_unique;
+    g.memo2 = memo && dbl ? memo : nullptr;
+    g.memo3 = memo && dbl ? memo + (1 << kLogMemo) : nullptr;
     uint32_t blocked;
     const Node s0 = node_from_bytes(bv, pl, blocked);
     g.blocked = blocked;
@@ -198,7 +204,8 @@ __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint6
 
 // Roll + movegen + obs for one lane according to its `need` byte
 // (reset: backgammon_env.py:78-113; pass/turn: :183-188 roll_dice + update_legal_moves).
-__device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4* lds_tab) {
+template <int LOG>
+__device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4* lds_tab, uint4* lds_memo) {
     const int need = rd(bv, R_NEED);
     if (need == NEED_NONE) return bv;
     Rng rng;
@@ -234,8 +241,8 @@ __device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4
     const int cur = rd(bv, R_CUR);
     int total;
     bool ovf;
-    int n = run_movegen<kLogSlots>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves, A.max_moves, lds_tab,
-                                   kCapFast, &total, &ovf);
+    int n = run_movegen<LOG>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves, A.max_moves, lds_tab,
+                             cap_fast<LOG>(), &total, &ovf, lds_memo);
     int flags = rd(bv, R_FLAGS) & ~1;
     if (ovf) {
         if (lane_id() == 0) { const int q = atomicAdd(A.ovf_count, 1); A.ovf_queue[q] = gi; }
@@ -327,28 +334,31 @@ __device__ __forceinline__ void store_rec(const Args& A, int gi, int bv) { A.lan
 
 // -------------------------------------------------------------- kernels --
 // PHASE 0: apply + advance fused (per-lane dice); 1: apply only; 2: advance only.
-template <int PHASE>
+template <int PHASE, int LOG>
 __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
                                              int32_t* info) {
-    __shared__ uint4 tab[1 << kLogSlots];
+    __shared__ uint4 tab[1 << LOG];
+    __shared__ uint4 memo[2 << kLogMemo];
     const int gi = blockIdx.x;
     int bv = load_rec(A, gi);
     if (PHASE != 2) bv = apply_lane(bv, gi, (int)ufl((uint32_t)actions[gi]), A, reward, done, info);
     if (PHASE != 1) {
-        bv = advance_lane(bv, gi, A, tab);
+        bv = advance_lane<LOG>(bv, gi, A, tab, memo);
         if (obs) write_obs(bv, obs + (size_t)gi * 198);
     }
     store_rec(A, gi, bv);
 }
 
+template <int LOG>
 __global__ __launch_bounds__(64) void k_reset(Args A, const uint8_t* lane_mask, float* obs, int mark_only) {
-    __shared__ uint4 tab[1 << kLogSlots];
+    __shared__ uint4 tab[1 << LOG];
+    __shared__ uint4 memo[2 << kLogMemo];
     const int gi = blockIdx.x;
     int bv = load_rec(A, gi);
     const bool sel = lane_mask == nullptr || ufl(lane_mask[gi]) != 0u;
     if (sel) bv = wr(bv, R_NEED, NEED_RESET);
     if (!mark_only) {
-        bv = advance_lane(bv, gi, A, tab);
+        bv = advance_lane<LOG>(bv, gi, A, tab, memo);
         if (obs) write_obs(bv, obs + (size_t)gi * 198);
     }
     store_rec(A, gi, bv);
@@ -386,10 +396,12 @@ __global__ __launch_bounds__(64) void k_shared_dice(Args A) {
 }
 
 // Standalone get_all_possible_moves on arbitrary boards.
+template <int LOG>
 __global__ __launch_bounds__(64) void k_movegen(const int8_t* boards, const uint8_t* players, const uint8_t* dice,
                                                 int n, int cap, int16_t* nmoves, int32_t* ntotal, uint64_t* moves,
                                                 int32_t* ovf_count, int32_t* ovf_queue) {
-    __shared__ uint4 tab[1 << kLogSlots];
+    __shared__ uint4 tab[1 << LOG];
+    __shared__ uint4 memo[2 << kLogMemo];
     const int gi = blockIdx.x;
     const int l = lane_id();
     const int bv = l < 52 ? (int)boards[(size_t)gi * 52 + l] : 0;
@@ -397,7 +409,7 @@ __global__ __launch_bounds__(64) void k_movegen(const int8_t* boards, const uint
     const int r0 = (int)ufl(dice[2 * gi]), r1 = (int)ufl(dice[2 * gi + 1]);
     int total;
     bool ovf;
-    int nm = run_movegen<kLogSlots>(bv, pl, r0, r1, moves + (size_t)gi * cap, cap, tab, kCapFast, &total, &ovf);
+    int nm = run_movegen<LOG>(bv, pl, r0, r1, moves + (size_t)gi * cap, cap, tab, cap_fast<LOG>(), &total, &ovf, memo);
     if (ovf) {
         if (l == 0) { const int q = atomicAdd(ovf_count, 1); ovf_queue[q] = gi; }
         nm = 0; total = 0;
@@ -411,6 +423,7 @@ template <int SRC>
 __global__ __launch_bounds__(64) void k_movegen_slow(Args A, const int8_t* boards, const uint8_t* players,
                                                      const uint8_t* dice, int cap, int16_t* nmoves, int32_t* ntotal,
                                                      uint64_t* moves, uint4* tables) {
+    __shared__ uint4 memo[2 << kLogMemo];
     uint4* tab = tables + ((size_t)blockIdx.x << kLogSlotsSlow);
     const int count = (int)ufl((uint32_t)*A.ovf_count);
     for (int q = blockIdx.x; q < count; q += gridDim.x) {
@@ -427,7 +440,7 @@ __global__ __launch_bounds__(64) void k_movegen_slow(Args A, const int8_t* board
         const int c = SRC == 0 ? A.max_moves : cap;
         int total;
         bool ovf;
-        int nm = run_movegen<kLogSlotsSlow>(bv, pl, r0, r1, out, c, tab, kCapSlow, &total, &ovf);
+        int nm = run_movegen<kLogSlotsSlow>(bv, pl, r0, r1, out, c, tab, kCapSlow, &total, &ovf, memo);
         if (ovf) { if (l == 0) atomicOr(A.err, 1); nm = 0; total = 0; }
         if (SRC == 0) {
             bv = wr(bv, R_NM0, nm & 0xFF);
@@ -508,15 +521,17 @@ __global__ void k_action_masks(Args A, int16_t* counts, float* masks) {
 }
 
 // Re-enumerate the legal moves of caller-posed lanes (bgx_set_lanes).
+template <int LOG>
 __global__ __launch_bounds__(64) void k_regen(Args A, int lane0) {
-    __shared__ uint4 tab[1 << kLogSlots];
+    __shared__ uint4 tab[1 << LOG];
+    __shared__ uint4 memo[2 << kLogMemo];
     const int gi = lane0 + blockIdx.x;
     int bv = load_rec(A, gi);
     const int cur = rd(bv, R_CUR), r0 = rd(bv, R_ROLL0), r1 = rd(bv, R_ROLL1);
     int total;
     bool ovf;
-    int n = run_movegen<kLogSlots>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves, A.max_moves, tab, kCapFast,
-                                   &total, &ovf);
+    int n = run_movegen<LOG>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves, A.max_moves, tab, cap_fast<LOG>(),
+                             &total, &ovf, memo);
     int flags = rd(bv, R_FLAGS) & ~1;
     if (ovf) {
         if (lane_id() == 0) { const int q = atomicAdd(A.ovf_count, 1); A.ovf_queue[q] = gi; }
@@ -553,6 +568,7 @@ int fail(hipError_t e, int code = BGX_EDEVICE) {
 
 struct bgx_engine {
     int device;
+    int lds_log;      // 9 or 10
     Args a;
     uint4* slow_tables;
     int slow_waves;
@@ -560,6 +576,11 @@ struct bgx_engine {
 };
 
 #define CK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return fail(_e); } while (0)
+#define LAUNCH_LOG(e, K, grid, s, ...)                                                            \
+    do {                                                                                          \
+        if ((e)->lds_log == 9) hipLaunchKernelGGL(K<9>, grid, dim3(64), 0, s, __VA_ARGS__);       \
+        else hipLaunchKernelGGL(K<10>, grid, dim3(64), 0, s, __VA_ARGS__);                        \
+    } while (0)
 #define CKL() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return fail(_e); } while (0)
 
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
@@ -585,6 +606,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     memset(&e->a, 0, sizeof e->a);
     e->device = device;
     e->seed = seed;
+    const char* ll = getenv("BGX_LDS_LOG");
+    e->lds_log = (ll && atoi(ll) == 9) ? 9 : 10;
     Args& A = e->a;
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
@@ -679,11 +702,11 @@ int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void*
     CK(hipSetDevice(e->device));
     CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
     if (A.dice_mode == BGX_DICE_MT_SHARED) {
-        hipLaunchKernelGGL(k_reset, dim3(A.B), dim3(64), 0, s, A, lane_mask_dev, obs_dev, 1);
+        LAUNCH_LOG(e, k_reset, dim3(A.B), s, A, lane_mask_dev, obs_dev, 1);
         hipLaunchKernelGGL(k_shared_dice, dim3(1), dim3(64), 0, s, A);
-        hipLaunchKernelGGL(k_reset, dim3(A.B), dim3(64), 0, s, A, nullptr, obs_dev, 0);
+        LAUNCH_LOG(e, k_reset, dim3(A.B), s, A, nullptr, obs_dev, 0);
     } else {
-        hipLaunchKernelGGL(k_reset, dim3(A.B), dim3(64), 0, s, A, lane_mask_dev, obs_dev, 0);
+        LAUNCH_LOG(e, k_reset, dim3(A.B), s, A, lane_mask_dev, obs_dev, 0);
     }
     CKL();
     return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
@@ -697,11 +720,22 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     CK(hipSetDevice(e->device));
     CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
     if (A.dice_mode == BGX_DICE_MT_SHARED) {
-        hipLaunchKernelGGL(k_step<1>, dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+        hipLaunchKernelGGL((k_step<1, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
+                           info_dev);
         hipLaunchKernelGGL(k_shared_dice, dim3(1), dim3(64), 0, s, A);
-        hipLaunchKernelGGL(k_step<2>, dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+        if (e->lds_log == 9)
+            hipLaunchKernelGGL((k_step<2, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
+                               info_dev);
+        else
+            hipLaunchKernelGGL((k_step<2, 10>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev,
+                               done_dev, info_dev);
     } else {
-        hipLaunchKernelGGL(k_step<0>, dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+        if (e->lds_log == 9)
+            hipLaunchKernelGGL((k_step<0, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
+                               info_dev);
+        else
+            hipLaunchKernelGGL((k_step<0, 10>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev,
+                               done_dev, info_dev);
     }
     CKL();
     return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
@@ -717,8 +751,8 @@ int bgx_movegen(bgx_engine* e, const int8_t* boards52_dev, const uint8_t* player
     hipStream_t s = (hipStream_t)stream;
     CK(hipSetDevice(e->device));
     CK(hipMemsetAsync(e->a.ovf_count, 0, 16, s));
-    hipLaunchKernelGGL(k_movegen, dim3(n), dim3(64), 0, s, boards52_dev, players_dev, dice_dev, n, max_moves,
-                       n_moves_dev, n_total_dev, moves_dev, e->a.ovf_count, e->a.ovf_queue);
+    LAUNCH_LOG(e, k_movegen, dim3(n), s, boards52_dev, players_dev, dice_dev, n, max_moves, n_moves_dev, n_total_dev,
+               moves_dev, e->a.ovf_count, e->a.ovf_queue);
     CKL();
     return slow_path(e, s, 1, boards52_dev, players_dev, dice_dev, max_moves, n_moves_dev, n_total_dev, moves_dev);
 }
@@ -782,7 +816,7 @@ int bgx_set_lanes(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_
     CK(hipSetDevice(e->device));
     CK(hipMemcpyAsync(A.lanes + (size_t)lane0 * 64, lanes_src, (size_t)n * 64, hipMemcpyDeviceToDevice, s));
     CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
-    hipLaunchKernelGGL(k_regen, dim3(n), dim3(64), 0, s, A, lane0);
+    LAUNCH_LOG(e, k_regen, dim3(n), s, A, lane0);
     CKL();
     return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
 }

@@ -35,8 +35,20 @@ for s in stats[:12]:
         k["WRITE_SIZE_KiB"] = statistics.mean(w)
         k["hbm_bytes_per_launch"] = (2 * k["FETCH_SIZE_KiB"] + k["WRITE_SIZE_KiB"]) * 1024
     kernels.append(k)
+# per-dispatch durations of the dominant kernels over the timed tail (last --steps launches)
+tail = None
+for tok in cmd.split():
+    pass
+args = cmd.split()
+if "--steps" in args:
+    tail = int(args[args.index("--steps") + 1])
+trace = list(csv.DictReader(open(os.path.join(out, "trace", "run_kernel_trace.csv"))))
+for k in kernels[:4]:
+    d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in trace if r["Kernel_Name"] == k["name"]]
+    if tail and len(d) >= tail:
+        k["avg_ns_timed_tail"] = statistics.mean(d[-tail:])
 summary = {"command": "python bench.py " + cmd, "kernels": kernels}
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
 for k in kernels:
-    print(f"{k['pct']:6.2f}% {k['avg_ns']/1e3:10.1f} us x{k['calls']:4d}  {k['name'][:80]}  "
-          f"{k.get('hbm_bytes_per_launch', 0)/1e6:.1f} MB")
+    print(f"{k['pct']:6.2f}% {k['avg_ns']/1e3:10.1f} us (tail {k.get('avg_ns_timed_tail', 0)/1e3:.1f}) "
+          f"x{k['calls']:4d}  {k['name'][:70]}  {k.get('hbm_bytes_per_launch', 0)/1e6:.1f} MB")
