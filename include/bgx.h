@@ -152,6 +152,29 @@ int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed_de
                    uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out, float* value_out,
                    float* logits_out, void* stream);
 
+/* ---- value head search: V(x) = value_head(relu(fc1 x)), H <= 64 ----
+ * bgx_value_pack packs fc1.weight [H][198], fc1.bias [H], value_head.weight [H],
+ * value_head.bias [1] into bgx_value_packed_size(H) floats (MFMA operand order);
+ * value_bias is value_head.bias[0] passed by value. */
+int bgx_value_packed_size(int32_t hidden);
+int bgx_value_pack(const float* W1, const float* b1, const float* wv, const float* bv, int32_t hidden,
+                   float* packed_dev, void* stream);
+
+/* 1-ply greedy over every lane's legal afterstates (features with the mover's
+ * one-hot, as legal_board_features, backgammon_env.py:207-216): best_out int32[B]
+ * = first argmax V, bestv_out float[B], values_out float[B][max_moves] (may be NULL). */
+int bgx_one_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float value_bias, int32_t* best_out,
+                float* bestv_out, float* values_out, void* stream);
+
+/* 2-ply expectimax over the 21 rolls (get_all_dice_rolls.py:5-34) for every lane:
+ * Q(a) = sum_r p_r min_{opponent replies b} V(enc(b, opponent)), leaf = a when the
+ * opponent cannot move; best_out = first argmax Q.  q_out float[B][max_moves] and
+ * bestq_out may be NULL; stats_host (may be NULL) receives {leaves evaluated,
+ * (afterstate, roll) jobs, afterstates}.  Synchronises the stream (sizes its
+ * workspace from the afterstate count). */
+int bgx_two_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float value_bias, int32_t* best_out,
+                float* bestq_out, float* q_out, uint64_t* stats_host, void* stream);
+
 /* Last HIP error string of this thread (diagnostics). */
 const char* bgx_last_error(void);
 

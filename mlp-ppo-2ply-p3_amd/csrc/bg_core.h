@@ -175,14 +175,25 @@ __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b
 constexpr int kLogMemo = 8;
 constexpr int kMemoCap = (7 << kLogMemo) / 8;
 
-template <int LOG_SLOTS, typename SlotPtr>
+// Where surviving entries go.  MoveSink: the env's ordered move list in HBM
+// (first `cap` entries).  Other sinks (bg_search.hip) keep afterstate keys.
+struct MoveSink {
+    uint64_t* out;      // this game's move list, `cap` entries
+    int cap;
+    __device__ __forceinline__ void reset() {}
+    __device__ __forceinline__ void push(const Node&, uint64_t enc, int idx) {
+        if (idx < cap && (threadIdx.x & 63) == 0) out[idx] = enc;
+    }
+};
+
+template <int LOG_SLOTS, typename SlotPtr, typename Sink = MoveSink>
 struct Gen {
     SlotPtr tab;
     uint4* memo2;       // LDS memo tables (nullptr = no pruning)
     uint4* memo3;
     int n_memo2, n_memo3;
-    uint64_t* out;      // this game's move list, `cap` entries
-    int cap, pl;
+    Sink sink;
+    int pl;
     uint32_t blocked;
     int cur_max, count, n_unique, cap_unique;
     bool ovf;
@@ -191,9 +202,9 @@ struct Gen {
         const uint32_t a = (uint32_t)s.lo, b = (uint32_t)(s.lo >> 32);
         if (!table_insert<LOG_SLOTS>(tab, a, b, s.hi, s.k3)) return;
         if (++n_unique >= cap_unique) { ovf = true; return; }
-        if (len > cur_max) { cur_max = len; count = 0; }
+        if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
-            if (count < cap && (threadIdx.x & 63) == 0) out[count] = enc;
+            sink.push(s, enc, count);
             ++count;
         }
     }

@@ -1,0 +1,93 @@
+"""1-ply / 2-ply search kernels vs a composition of the oracle (move lists,
+afterstates, features) and the torch fp32 value head.  Tolerance 1e-5 on V and Q."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+ROLLS = [(a, b) for a in range(1, 7) for b in range(a, 7)]
+PROBS = np.array([1 / 36 if a == b else 2 / 36 for a, b in ROLLS], np.float32)
+
+
+@pytest.fixture(scope="module")
+def setup(golden):
+    import bgx
+    from bgx.policy import PolicyNet
+    from bgx.search import ValueHead
+    mlp = golden("mlp")
+    net = PolicyNet(hidden_size=40).cuda()
+    net.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in mlp.items()
+                         if k.startswith("h40_") and not k.endswith(("logits", "values"))})
+    B = 48
+    eng = bgx.Engine(batch=B, max_moves=500, dice="mt", auto_reset=True)
+    eng.seed(np.arange(500, 500 + B, dtype=np.uint32))
+    eng.reset()
+    rng = np.random.RandomState(2)
+    for _ in range(25):
+        nm = eng.n_moves().cpu().numpy()
+        eng.step(torch.from_numpy(np.array([rng.randint(k) if k else 0 for k in nm], np.int32)).cuda())
+    return bgx, net, ValueHead(net), eng
+
+
+def _V(net, feats):
+    with torch.no_grad():
+        return net(torch.from_numpy(np.asarray(feats, np.float32)).cuda())[1].cpu().numpy()
+
+
+def test_one_ply(setup):
+    bgx, net, vh, eng = setup
+    from bgx.search import one_ply
+    best, bestv, vals = one_ply(eng, vh, want_values=True)
+    feats = eng.legal_features().cpu().numpy()
+    n = eng.n_moves().cpu().numpy()
+    best, vals = best.cpu().numpy(), vals.cpu().numpy()
+    for i in range(eng.batch):
+        if n[i] == 0:
+            continue
+        v = _V(net, feats[i, :n[i]])
+        assert np.abs(vals[i, :n[i]] - v).max() < TOL
+        assert best[i] == int(np.argmax(vals[i, :n[i]]))
+
+
+def test_two_ply_vs_oracle_composition(setup):
+    bgx, net, vh, eng = setup
+    from bgx.search import two_ply
+    best, bestq, q, stats = two_ply(eng, vh, want_q=True)
+    rec, mv, _ = eng.lanes()
+    rec, mv = rec.cpu().numpy(), mv.cpu().numpy().view(np.uint64)
+    q, best = q.cpu().numpy(), best.cpu().numpy()
+    n_all = eng.n_moves().cpu().numpy()
+    leaves = 0
+    checked = 0
+    for i in range(eng.batch):
+        n = int(n_all[i])
+        board, mover = rec[i, :52].view(np.int8), int(rec[i, 52])
+        opp = 1 - mover
+        if n == 0:
+            continue
+        if checked < 10:
+            Q = np.zeros(n, np.float32)
+            for a in range(n):
+                aft = O.apply_move(board, mover, int(mv[i, a]))
+                acc = 0.0
+                for r, roll in enumerate(ROLLS):
+                    reps, cnt = O.movegen(aft, opp, roll, cap=4096)
+                    if cnt == 0:
+                        leaf = [O.features(aft, opp)]
+                    else:
+                        leaf = [O.features(O.apply_move(aft, opp, int(b)), opp) for b in reps]
+                    acc += float(PROBS[r]) * float(_V(net, leaf).min())
+                Q[a] = acc
+            assert np.abs(q[i, :n] - Q).max() < TOL, i
+            assert abs(Q[best[i]] - Q.max()) < TOL
+            checked += 1
+        for a in range(n):
+            aft = O.apply_move(board, mover, int(mv[i, a]))
+            for roll in ROLLS:
+                leaves += max(O.movegen(aft, opp, roll, cap=4096)[1], 1)
+    assert checked == 10
+    assert stats["leaves"] == leaves
+    assert stats["afterstates"] == int(n_all.sum()) and stats["jobs"] == 21 * int(n_all.sum())
