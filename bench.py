@@ -33,7 +33,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c1"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c1", "c2"])
+    ap.add_argument("--two-ply-batches", type=int, default=1,
+                    help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--burn-in", type=int, default=150,
                     help="untimed steps before warmup so the game population reaches its steady mix "
@@ -103,6 +105,36 @@ def cpu_baseline(seconds: float):
     return {"value": steps / el, "unit": "env steps/s", "cores": 1, "kind": "port",
             "sample": f"{steps} random-policy BackgammonEnv.step calls of the C oracle (oracle/bgoracle.c), "
                       f"1 thread, {el:.1f} s"}
+
+
+def two_ply_bench(eng, batches: int, ws: int, dev):
+    """C4: 2-ply expectimax over the 21 rolls for every lane's current position
+    (B roots per GPU), value head MLP(198->40->1) on MFMA."""
+    from bgx.policy import PolicyNet
+    from bgx.search import ValueHead, two_ply
+    torch.manual_seed(1)
+    vnet = PolicyNet(hidden_size=40).to(dev)
+    vh = ValueHead(vnet)
+    two_ply(eng, vh)                               # warm (workspace sizing, code load)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    t0 = time.perf_counter()
+    leaves = jobs = 0
+    for _ in range(batches):
+        _, _, _, st = two_ply(eng, vh)
+        leaves += st["leaves"]
+        jobs += st["jobs"]
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    el = max_over_ranks(time.perf_counter() - t0, ws)
+    roots = sum_over_ranks(float(eng.batch * batches), ws)
+    leaves_all = sum_over_ranks(float(leaves), ws)
+    flop_per_leaf = 2 * 198 * 40 + 2 * 40
+    return {"config": "C4: B=65536 roots/GPU, 2-ply expectimax over 21 rolls, value MLP 198->40->1 (f32 MFMA)",
+            "root_decisions_per_s": roots / el, "leaf_evals_per_s": leaves_all / el,
+            "leaves_per_root": leaves_all / roots, "reply_enumerations": jobs * ws, "seconds": el,
+            "mfma_achieved_tflops": leaves_all * flop_per_leaf / el / 1e12,
+            "mfma_peak_tflops_f32": 157.3}
 
 
 def main():
@@ -226,6 +258,8 @@ def main():
                      "kernel_ms": kern_ms, "bytes_per_lane_step": bytes_per_lane,
                      "mean_legal_moves": mean_moves},
     }
+    if args.two_ply_batches > 0:
+        line["two_ply"] = two_ply_bench(eng, args.two_ply_batches, ws, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

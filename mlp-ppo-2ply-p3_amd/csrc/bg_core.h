@@ -157,6 +157,23 @@ __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b
     }
 }
 
+// Per-lane (divergent) membership test along the same linear probe sequence.
+template <int LOG_SLOTS, typename SlotPtr>
+__device__ __forceinline__ bool table_contains_lane(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
+    uint32_t h = key_hash(a, b, c, d) & mask;
+    for (;;) {
+        const uint4 v = tab[h];
+        if (v.x == a && v.y == b && v.z == c && v.w == d) return true;
+        if ((v.x | v.y | v.z | v.w) == 0u) return false;
+        h = (h + 1u) & mask;
+    }
+}
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
 // ------------------------------------------------------------ enumeration --
 // Filtered-list bookkeeping (filter_full_moves_by_max_submoves,
 // get_all_moves.py:73-94): entries shorter than the running maximum can never
@@ -209,6 +226,43 @@ struct Gen {
         }
     }
 
+    // All children of node s (list k, die d) as entries prefix | enc << shift of
+    // length len, in child order.  Children of one node are pairwise distinct
+    // afterstates (different source points), so their duplicate checks against
+    // the set as it stood before the batch run one child per lane; only the new
+    // ones are then inserted, serially and in child order -- the same set, list
+    // order and counts as the reference's one-by-one add_unique_board calls.
+    __device__ __forceinline__ void leaf_batch(const Node& s, const Kids& k, int d, uint64_t prefix, int shift,
+                                               int len) {
+        const int l = threadIdx.x & 63;
+        const bool act = l < 32 && ((k.bits >> l) & 1u);
+        uint32_t ka = 0, kb = 0, kc = 0, kd = 0, ke = 0;
+        bool fresh = false;
+        if (act) {
+            const Sub m = child(s, k, l, d, pl);
+            const Node t = apply(s, m, pl);
+            ka = (uint32_t)t.lo; kb = (uint32_t)(t.lo >> 32); kc = t.hi; kd = t.k3; ke = m.enc;
+            fresh = !table_contains_lane<LOG_SLOTS>(tab, ka, kb, kc, kd);
+        }
+        uint64_t nm = __ballot(fresh);
+        while (nm) {
+            const int src = __ffsll((unsigned long long)nm) - 1;
+            nm &= nm - 1;
+            Node t;
+            t.lo = (uint64_t)rdl(ka, src) | ((uint64_t)rdl(kb, src) << 32);
+            t.hi = rdl(kc, src);
+            t.k3 = rdl(kd, src);
+            const uint32_t enc = rdl(ke, src);
+            table_insert<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3);
+            if (++n_unique >= cap_unique) { ovf = true; return; }
+            if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
+            if (len == cur_max) {
+                sink.push(t, prefix | ((uint64_t)enc << shift), count);
+                ++count;
+            }
+        }
+    }
+
     // handle_non_doubles (handle_moves.py:109-200)
     __device__ __forceinline__ void pass_nd(const Node& s0, int da, int db) {
         const Kids k1 = gen(s0, da, pl, blocked);
@@ -223,11 +277,7 @@ struct Gen {
             const Node s1 = apply(s0, m1, pl);
             if (exists) {
                 const Kids k2 = gen(s1, db, pl, blocked);
-                for (uint32_t b2 = k2.bits; b2; b2 &= b2 - 1u) {
-                    const Sub m2 = child(s1, k2, __builtin_ctz(b2), db, pl);
-                    insert(apply(s1, m2, pl), (uint64_t)m1.enc | ((uint64_t)m2.enc << 16), 2);
-                    if (ovf) return;
-                }
+                if (k2.bits) { leaf_batch(s1, k2, db, (uint64_t)m1.enc, 16, 2); if (ovf) return; }
             } else {
                 insert(s1, (uint64_t)m1.enc, 1);
                 if (ovf) return;
@@ -268,9 +318,8 @@ struct Gen {
                     const uint64_t e3 = e2 | ((uint64_t)m3.enc << 32);
                     const Kids k4 = gen(s3, d, pl, blocked);
                     if (!k4.bits && !got4) { insert(s3, e3, 3); if (ovf) return; }
-                    for (uint32_t b4 = k4.bits; b4; b4 &= b4 - 1u) {
-                        const Sub m4 = child(s3, k4, __builtin_ctz(b4), d, pl);
-                        insert(apply(s3, m4, pl), e3 | ((uint64_t)m4.enc << 48), 4);
+                    if (k4.bits) {
+                        leaf_batch(s3, k4, d, e3, 48, 4);
                         if (ovf) return;
                         got4 = true;
                     }
