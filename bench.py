@@ -226,11 +226,16 @@ def main():
     # record in+out 128, action 4, chosen move 8, new move list 8*n, reward 4, done 1, rng ctr 8+8
     bytes_per_lane = 128 + 4 + 8 + 8 * mean_moves + 4 + 1 + 16
     achieved = B * bytes_per_lane / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_step_traffic.json")
+    # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
+    # (tools/profile.sh -> profiles/latest_summary.json; (2*FETCH_SIZE + WRITE_SIZE)*1024)
+    traffic, traffic_src = None, None
+    prof = os.path.join(ROOT, "profiles", "latest_summary.json")
     if os.path.exists(prof):
         try:
-            traffic = json.load(open(prof)).get("bytes_per_launch")
+            summ = json.load(open(prof))
+            for k in summ["kernels"]:
+                if "k_step<0" in k["name"] and "hbm_bytes_per_launch" in k:
+                    traffic, traffic_src = k["hbm_bytes_per_launch"], summ.get("command")
         except Exception:
             traffic = None
     line = {
@@ -254,7 +259,8 @@ def main():
                    "parallelism": f"dp{ws} (independent game shards)"},
         "roofline": {"kernel": "k_step<0> (apply + dice + move enumeration + dedup, one wave per game)",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": B * bytes_per_lane,
                      "kernel_ms": kern_ms, "bytes_per_lane_step": bytes_per_lane,
                      "mean_legal_moves": mean_moves},
     }

@@ -110,17 +110,24 @@ __global__ __launch_bounds__(64) void k_movegen(const int8_t* boards, const uint
     if (l == 0) { nmoves[gi] = (int16_t)nm; if (ntotal) ntotal[gi] = total; }
 }
 
-// Slow path for positions whose dedup set outgrew the LDS table: same code,
-// 2 MiB table in HBM per wave.  SRC 0 = engine lanes, 1 = standalone arrays.
-template <int SRC>
-__global__ __launch_bounds__(64) void k_movegen_slow(Args A, const int8_t* boards, const uint8_t* players,
+// Overflow tiers for positions whose dedup set outgrew the main LDS table
+// (cap 7/8 of 2^LOG slots).  Tier 1: the same code with a 4,096-slot (64 KiB)
+// LDS table, fed by queue 1; anything larger (> 3,584 distinct afterstates)
+// moves to queue 2 = tier 2, a 131,072-slot table in HBM per wave.  Every
+// position stays exact.  SRC 0 = engine lanes, 1 = standalone arrays.
+constexpr int kLogMid = 12;
+
+template <int SRC, int TIER>
+__global__ __launch_bounds__(64) void k_movegen_over(Args A, const int8_t* boards, const uint8_t* players,
                                                      const uint8_t* dice, int cap, int16_t* nmoves, int32_t* ntotal,
                                                      uint64_t* moves, uint4* tables) {
     __shared__ uint4 memo[2 << kLogMemo];
-    uint4* tab = tables + ((size_t)blockIdx.x << kLogSlotsSlow);
-    const int count = (int)ufl((uint32_t)*A.ovf_count);
+    __shared__ uint4 lds_tab[TIER == 1 ? (1 << kLogMid) : 1];
+    uint4* tab = TIER == 1 ? lds_tab : tables + ((size_t)blockIdx.x << kLogSlotsSlow);
+    const int count = (int)ufl((uint32_t)A.ovf_count[TIER - 1]);
+    const int32_t* queue = A.ovf_queue + (TIER == 1 ? 0 : A.B);
     for (int q = blockIdx.x; q < count; q += gridDim.x) {
-        const int gi = (int)ufl((uint32_t)A.ovf_queue[q]);
+        const int gi = (int)ufl((uint32_t)queue[q]);
         const int l = lane_id();
         int bv, pl, r0, r1;
         if (SRC == 0) {
@@ -133,8 +140,19 @@ __global__ __launch_bounds__(64) void k_movegen_slow(Args A, const int8_t* board
         const int c = SRC == 0 ? A.max_moves : cap;
         int total;
         bool ovf;
-        int nm = run_movegen<kLogSlotsSlow>(bv, pl, r0, r1, out, c, tab, kCapSlow, &total, &ovf, memo);
-        if (ovf) { if (l == 0) atomicOr(A.err, 1); nm = 0; total = 0; }
+        int nm;
+        if (TIER == 1)
+            nm = run_movegen<kLogMid>(bv, pl, r0, r1, out, c, lds_tab, cap_fast<kLogMid>(), &total, &ovf, memo);
+        else
+            nm = run_movegen<kLogSlotsSlow>(bv, pl, r0, r1, out, c, tab, kCapSlow, &total, &ovf, memo);
+        if (ovf) {
+            if (TIER == 1) {
+                if (l == 0) { const int q2 = atomicAdd(A.ovf_count + 1, 1); A.ovf_queue[A.B + q2] = gi; }
+                continue;
+            }
+            if (l == 0) atomicOr(A.err, 1);
+            nm = 0; total = 0;
+        }
         if (SRC == 0) {
             bv = wr(bv, R_NM0, nm & 0xFF);
             bv = wr(bv, R_NM1, (nm >> 8) & 0xFF);
@@ -273,12 +291,17 @@ int bgx_internal_fail(hipError_t e) { return fail(e); }
 
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
                      const uint8_t* dice, int cap, int16_t* nm, int32_t* nt, uint64_t* moves) {
-    if (src == 0)
-        hipLaunchKernelGGL(k_movegen_slow<0>, dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice, cap,
-                           nm, nt, moves, e->slow_tables);
-    else
-        hipLaunchKernelGGL(k_movegen_slow<1>, dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice, cap,
-                           nm, nt, moves, e->slow_tables);
+    if (src == 0) {
+        hipLaunchKernelGGL((k_movegen_over<0, 1>), dim3(256), dim3(64), 0, s, e->a, boards, players, dice, cap, nm, nt,
+                           moves, e->slow_tables);
+        hipLaunchKernelGGL((k_movegen_over<0, 2>), dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice,
+                           cap, nm, nt, moves, e->slow_tables);
+    } else {
+        hipLaunchKernelGGL((k_movegen_over<1, 1>), dim3(256), dim3(64), 0, s, e->a, boards, players, dice, cap, nm, nt,
+                           moves, e->slow_tables);
+        hipLaunchKernelGGL((k_movegen_over<1, 2>), dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice,
+                           cap, nm, nt, moves, e->slow_tables);
+    }
     CKL();
     return BGX_OK;
 }
@@ -311,7 +334,7 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     alloc((void**)&A.ctr, B * 8);
     alloc((void**)&A.shared_rolls, B * 4);
     alloc((void**)&A.ovf_count, 16);
-    alloc((void**)&A.ovf_queue, B * 4);
+    alloc((void**)&A.ovf_queue, 2 * B * 4);
     alloc((void**)&A.err, 16);
     alloc((void**)&e->slow_tables, (size_t)kSlowWaves * ((size_t)16 << kLogSlotsSlow));
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }

@@ -11,3 +11,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python bench.py "$@" > $OUT/fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python bench.py "$@" > $OUT/write.log 2>&1
 python tools/summarize_profile.py $OUT "$*"
+cp $OUT/summary.json gpurun_out/$TAG.summary.json
+cp $OUT/trace/run_kernel_stats.csv gpurun_out/$TAG.kernel_stats.csv
