@@ -33,7 +33,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c1", "c2"])
+    ap.add_argument("--workload", default="c3", choices=["c3", "c1"])
+    ap.add_argument("--horizon", type=int, default=32,
+                    help="also time full PPO iterations (T rollout steps + update); 0 = skip")
     ap.add_argument("--two-ply-batches", type=int, default=1,
                     help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
     ap.add_argument("--batch", type=int, default=65536)
@@ -105,6 +107,28 @@ def cpu_baseline(seconds: float):
     return {"value": steps / el, "unit": "env steps/s", "cores": 1, "kind": "port",
             "sample": f"{steps} random-policy BackgammonEnv.step calls of the C oracle (oracle/bgoracle.c), "
                       f"1 thread, {el:.1f} s"}
+
+
+def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 2):
+    """Full PPO iterations (rollout of `horizon` steps on B lanes + 4-epoch update
+    with the gradient all-reduce across ranks): env steps/s INCLUDING the update."""
+    from bgx.train import PPOTrainer
+    group = None
+    tr = PPOTrainer(batch=B, horizon=horizon, seed=11, device=dev, process_group=group)
+    tr.iteration()                                   # warm
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    t0 = time.perf_counter()
+    ms = [tr.iteration() for _ in range(iters)]
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    el = max_over_ranks(time.perf_counter() - t0, ws)
+    steps = sum_over_ranks(float(B * horizon * iters), ws)
+    return {"config": f"PPO iteration: B={B}/GPU x T={horizon} rollout + 4-epoch full-batch update "
+                      f"(chunked, features re-encoded from int8 records), grad all-reduce over {ws} rank(s)",
+            "env_steps_per_s_incl_update": steps / el, "seconds_per_iteration": el / iters,
+            "rollout_s": sum(m["rollout_s"] for m in ms) / iters, "update_s": sum(m["update_s"] for m in ms) / iters,
+            "losses_last": {k: ms[-1][k] for k in ("policy_loss", "value_loss", "entropy", "total_loss")}}
 
 
 def two_ply_bench(eng, batches: int, ws: int, dev):
@@ -266,6 +290,8 @@ def main():
     }
     if args.two_ply_batches > 0:
         line["two_ply"] = two_ply_bench(eng, args.two_ply_batches, ws, dev)
+    if args.horizon > 0 and args.workload in ("c3", "ppo"):
+        line["ppo_iteration"] = ppo_iteration_bench(B, args.horizon, ws, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -1,0 +1,250 @@
+"""GPU-resident PPO self-play trainer (the reference's train.py:30-123 loop,
+ppo_agent.py:218-366 update) on the bgx engine.
+
+Rollout: every step the fused policy kernel (bgx_policy_act) samples an
+action for all B lanes from their 64-byte lane records, the engine steps them,
+and the step's records / actions / log-probs / values / rewards / dones are
+kept in device buffers [T, B] (records are int8 boards: 64 B per sample instead
+of the reference's 792-byte fp32 observation); optionally mirrored to pinned
+host memory on a side stream.
+
+Update: returns, global normalisation, advantages = R_hat - V_old, then
+NUM_EPOCHS full-batch epochs exactly like ppo_agent.py:268-305 (autocast +
+GradScaler + Adam, clip 0.25, 0.5*MSE, -c_ent*H) but computed in chunks with
+gradient accumulation (features re-encoded from the stored records by the HIP
+encoder) and ONE all-reduce of the gradients per epoch across ranks.
+
+Returns: `returns="lane"` (default) discounts within each game lane;
+`returns="reference"` reproduces the reference's quirk of discounting over the
+flat step-major memory in which the environments are interleaved
+(ppo_agent.py:206-216).
+
+    python -m bgx.train --batch 65536 --horizon 64 --updates 10 [--metrics m.jsonl]
+    torchrun --nproc-per-node 8 -m bgx.train ...            (one process per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+from torch.amp import GradScaler, autocast
+
+from .engine import Engine, encode
+from .policy import PolicyNet, MASK_LOG
+from .ppo import (EPS_CLIP, GAMMA, LEARNING_RATE, NUM_EPOCHS, VALUE_LOSS_COEF, ENTROPY_COEF_START,
+                  ENTROPY_COEF_END, ENTROPY_ANNEAL_EPISODES, allreduce_mean_, global_normalize, _world)
+
+
+def lane_returns(rewards: torch.Tensor, dones: torch.Tensor, gamma: float = GAMMA) -> torch.Tensor:
+    """R_t = r_t + gamma * R_{t+1}, reset at done, per lane; [T, B] (vectorised over B)."""
+    T = rewards.shape[0]
+    out = torch.empty_like(rewards)
+    R = torch.zeros_like(rewards[0])
+    for t in range(T - 1, -1, -1):
+        R = torch.where(dones[t].bool(), torch.zeros_like(R), R)
+        R = rewards[t] + gamma * R
+        out[t] = R
+    return out
+
+
+def reference_returns(rewards: torch.Tensor, dones: torch.Tensor, gamma: float = GAMMA) -> torch.Tensor:
+    """ppo_agent.py:206-216 over the flat step-major memory (envs interleaved)."""
+    flat_r = rewards.reshape(-1).double().cpu().numpy()
+    flat_d = dones.reshape(-1).cpu().numpy()
+    out = [0.0] * len(flat_r)
+    R = 0.0
+    for k in range(len(flat_r) - 1, -1, -1):
+        if flat_d[k]:
+            R = 0.0
+        R = flat_r[k] + gamma * R
+        out[k] = R
+    return torch.tensor(out, dtype=torch.float32, device=rewards.device).view_as(rewards)
+
+
+def features_and_masks(records: torch.Tensor, n_actions: int):
+    feats = encode(records[:, :52].contiguous(), records[:, 52].contiguous())
+    counts = records[:, 60].to(torch.int32) | (records[:, 61].to(torch.int32) << 8)
+    legal = torch.arange(n_actions, device=records.device)[None, :] < counts[:, None]
+    return feats, legal
+
+
+def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_coef: float, group=None,
+              amp: bool = True):
+    """One full-batch PPO epoch (ppo_agent.py:268-305) over `chunks` =
+    iterable of (features, legal_mask, actions, old_logp, returns, advantages),
+    with gradient accumulation and one all-reduce.  Returns loss parts."""
+    optimizer.zero_grad(set_to_none=True)
+    parts = torch.zeros(4, dtype=torch.float64)
+    dev_type = next(net.parameters()).device.type
+    for feats, legal, actions, old_logp, returns, adv in chunks:
+        w = feats.shape[0] / n_total
+        with autocast(device_type=dev_type, enabled=amp):
+            logits, values = net(feats)
+            masked = torch.where(legal, logits.float(), logits.float() + MASK_LOG)
+            logp_all = torch.log_softmax(masked, dim=-1)
+            new_logp = logp_all.gather(1, actions.long()[:, None]).squeeze(1)
+            ratios = torch.exp(new_logp - old_logp)
+            surr1 = ratios * adv
+            surr2 = torch.clamp(ratios, 1 - EPS_CLIP, 1 + EPS_CLIP) * adv
+            policy_loss = -torch.min(surr1, surr2).mean()
+            value_loss = nn.functional.mse_loss(values.float().squeeze(-1), returns)
+            entropy = -(logp_all.exp() * logp_all).sum(-1).mean()
+            loss = policy_loss + VALUE_LOSS_COEF * value_loss - entropy_coef * entropy
+        scaler.scale(loss * w).backward()
+        parts += torch.tensor([policy_loss.item(), value_loss.item(), entropy.item(), loss.item()],
+                              dtype=torch.float64) * w
+    allreduce_mean_([p.grad for p in net.parameters() if p.grad is not None], group)
+    scaler.step(optimizer)
+    scaler.update()
+    return parts
+
+
+class PPOTrainer:
+    def __init__(self, batch: int = 65536, horizon: int = 64, hidden: int = 128, n_actions: int = 500,
+                 seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
+                 chunk: int = 1 << 20):
+        self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.group = process_group
+        self.rank = dist.get_rank(process_group) if _world(process_group) > 1 else 0
+        self.B, self.T, self.A = batch, horizon, n_actions
+        self.returns_mode = returns
+        self.chunk = chunk
+        self.eng = Engine(batch=batch, max_moves=n_actions, seed=seed * 1_000_003 + self.rank, dice="philox",
+                          auto_reset=True, device=self.dev)
+        torch.manual_seed(seed)
+        self.net = PolicyNet(hidden_size=hidden, action_size=n_actions).to(self.dev)
+        if _world(process_group) > 1:
+            for p in self.net.parameters():
+                dist.broadcast(p.data, src=0, group=process_group)
+        self.opt = torch.optim.Adam(self.net.parameters(), lr=LEARNING_RATE)
+        self.scaler = GradScaler(device=self.dev.type)
+        self.total_episodes = 0
+        self.entropy_coef = ENTROPY_COEF_START
+        self.step_counter = 0
+        self.seed = seed
+        T, B = horizon, batch
+        kw = dict(device=self.dev)
+        self.buf = {"records": torch.empty(T, B, 64, dtype=torch.uint8, **kw),
+                    "actions": torch.empty(T, B, dtype=torch.int32, **kw),
+                    "logp": torch.empty(T, B, dtype=torch.float32, **kw),
+                    "values": torch.empty(T, B, dtype=torch.float32, **kw),
+                    "rewards": torch.empty(T, B, dtype=torch.float32, **kw),
+                    "dones": torch.empty(T, B, dtype=torch.uint8, **kw)}
+        self.pinned = None
+        if pinned:
+            self.pinned = {k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in self.buf.items()}
+            self.copy_stream = torch.cuda.Stream(self.dev)
+        self.eng.reset(want_obs=False)
+
+    def rollout(self):
+        """T env steps on all B lanes (train.py:46-99 without the Python loops)."""
+        self.net.pack()
+        buf = self.buf
+        for t in range(self.T):
+            self.eng.records(out=buf["records"][t])
+            a, lp, v = self.net.act(buf["records"][t], seed=self.seed * 7919 + self.rank, step=self.step_counter)
+            self.step_counter += 1
+            buf["actions"][t].copy_(a)
+            buf["logp"][t].copy_(lp)
+            buf["values"][t].copy_(v)
+            _, r, d, _ = self.eng.step(a, want_obs=False, want_info=False)
+            buf["rewards"][t].copy_(r)
+            buf["dones"][t].copy_(d)
+            if self.pinned is not None:
+                cur = torch.cuda.current_stream(self.dev)
+                self.copy_stream.wait_stream(cur)
+                with torch.cuda.stream(self.copy_stream):
+                    for k in buf:
+                        self.pinned[k][t].copy_(buf[k][t], non_blocking=True)
+        eps = int(buf["dones"].sum().item())
+        if _world(self.group) > 1:
+            e = torch.tensor([eps], device=self.dev)
+            dist.all_reduce(e, group=self.group)
+            eps = int(e.item())
+        self.total_episodes += eps
+        return eps
+
+    def update(self):
+        """ppo_agent.py:218-366 on the device buffers."""
+        buf = self.buf
+        if self.returns_mode == "reference":
+            R = reference_returns(buf["rewards"], buf["dones"])
+        else:
+            R = lane_returns(buf["rewards"], buf["dones"])
+        R = global_normalize(R.reshape(-1), self.group)
+        adv = R - buf["values"].reshape(-1)
+        recs = buf["records"].reshape(-1, 64)
+        acts = buf["actions"].reshape(-1)
+        old = buf["logp"].reshape(-1)
+        N = recs.shape[0]
+
+        def chunks():
+            for s in range(0, N, self.chunk):
+                e = min(N, s + self.chunk)
+                f, legal = features_and_masks(recs[s:e], self.A)
+                yield f, legal, acts[s:e], old[s:e], R[s:e], adv[s:e]
+
+        parts = torch.zeros(4, dtype=torch.float64)
+        for _ in range(NUM_EPOCHS):
+            parts += ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group)
+        progress = min(1.0, self.total_episodes / ENTROPY_ANNEAL_EPISODES)       # ppo_agent.py:193-197
+        self.entropy_coef = ENTROPY_COEF_START - progress * (ENTROPY_COEF_START - ENTROPY_COEF_END)
+        p = (parts / NUM_EPOCHS).tolist()
+        return {"policy_loss": p[0], "value_loss": p[1], "entropy": p[2], "total_loss": p[3]}
+
+    def iteration(self):
+        t0 = time.perf_counter()
+        eps = self.rollout()
+        torch.cuda.synchronize(self.dev)
+        t1 = time.perf_counter()
+        m = self.update()
+        torch.cuda.synchronize(self.dev)
+        t2 = time.perf_counter()
+        ws = _world(self.group)
+        m.update({"episodes": eps, "env_steps": self.B * self.T * ws, "rollout_s": t1 - t0, "update_s": t2 - t1,
+                  "env_steps_per_s": self.B * self.T * ws / (t2 - t0), "entropy_coef": self.entropy_coef})
+        return m
+
+    def save(self, path: str):
+        torch.save(self.net.state_dict(), path)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--horizon", type=int, default=64)
+    ap.add_argument("--updates", type=int, default=10)
+    ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--metrics", default=None)
+    ap.add_argument("--save", default=None)
+    ap.add_argument("--returns", default="lane", choices=["lane", "reference"])
+    args = ap.parse_args()
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if ws > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    tr = PPOTrainer(batch=args.batch, horizon=args.horizon, hidden=args.hidden, seed=args.seed,
+                    returns=args.returns)
+    for u in range(args.updates):
+        m = tr.iteration()
+        m["update"] = u
+        if tr.rank == 0:
+            print(json.dumps(m), flush=True)
+            if args.metrics:
+                with open(args.metrics, "a") as f:
+                    f.write(json.dumps(m) + "\n")
+    if args.save and tr.rank == 0:
+        tr.save(args.save)
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

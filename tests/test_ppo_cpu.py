@@ -91,3 +91,89 @@ def test_two_rank_allreduce_equals_full_batch():
     (lin(X) ** 2).mean().backward()
     for g_ref, g0, g1 in zip([p.grad.numpy() for p in lin.parameters()], res[0][1], res[1][1]):
         assert np.allclose(g0, g_ref, atol=1e-6) and np.allclose(g1, g_ref, atol=1e-6)
+
+
+def test_returns_functions_match_reference_quirk():
+    from bgx.train import lane_returns, reference_returns
+    rng = np.random.RandomState(0)
+    T, B = 12, 5
+    r = torch.from_numpy(rng.choice([0.0, 0.0, 1.0, -1.0, 1.5], size=(T, B)).astype(np.float32))
+    d = torch.from_numpy((rng.rand(T, B) < 0.2).astype(np.uint8))
+    agent = BackgammonPPOAgent(action_size=500, device=torch.device("cpu"))
+    ref = np.array(agent.compute_returns(r.reshape(-1), d.reshape(-1).bool()), np.float32).reshape(T, B)
+    assert np.allclose(reference_returns(r, d).numpy(), ref, atol=1e-5)
+    lane = lane_returns(r, d).numpy()
+    for b in range(B):
+        R, exp = 0.0, np.zeros(T, np.float32)
+        for t in range(T - 1, -1, -1):
+            R = 0.0 if d[t, b] else R
+            R = float(r[t, b]) + 0.99 * R
+            exp[t] = R
+        assert np.allclose(lane[:, b], exp, atol=1e-5)
+
+
+def _epoch_inputs(n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    feats = torch.rand(n, 198, generator=g)
+    legal = torch.rand(n, 500, generator=g) < 0.1
+    legal[:, 0] = True
+    acts = torch.randint(0, 1, (n,), generator=g)
+    old = torch.log(torch.rand(n, generator=g) * 0.5 + 0.25)
+    ret = torch.randn(n, generator=g)
+    adv = torch.randn(n, generator=g)
+    return feats, legal, acts, old, ret, adv
+
+
+def _fresh_net():
+    from bgx.policy import PolicyNet
+    torch.manual_seed(5)
+    net = PolicyNet()
+    # SGD(lr=1): the parameter change IS the (all-reduced, unscaled) gradient, so the
+    # comparison below checks gradients (Adam's first step is ~lr*sign(g): ill-conditioned)
+    opt = torch.optim.SGD(net.parameters(), lr=1.0)
+    return net, opt, torch.amp.GradScaler(device="cpu")
+
+
+@pytest.mark.parametrize("amp,rtol,atol", [(False, 1e-4, 1e-6), (True, 2e-2, 2e-3)])
+def test_chunked_epoch_equals_full_batch(amp, rtol, atol):
+    """Gradient accumulation over chunks == one full-batch gradient (fp32 tight;
+    under the reference's autocast the tolerance is bf16's)."""
+    from bgx.train import ppo_epoch
+    data = _epoch_inputs(256)
+    net1, opt1, sc1 = _fresh_net()
+    ppo_epoch(net1, opt1, sc1, [data], 256, 0.15, amp=amp)
+    net2, opt2, sc2 = _fresh_net()
+    chunks = [tuple(x[i:i + 64] for x in data) for i in range(0, 256, 64)]
+    ppo_epoch(net2, opt2, sc2, chunks, 256, 0.15, amp=amp)
+    for a, b in zip(net1.parameters(), net2.parameters()):
+        assert torch.allclose(a, b, atol=atol, rtol=rtol)
+
+
+def _epoch_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=ws)
+    from bgx.train import ppo_epoch
+    data = _epoch_inputs(256)
+    net, opt, sc = _fresh_net()
+    shard = tuple(x[rank * 128:(rank + 1) * 128] for x in data)
+    ppo_epoch(net, opt, sc, [shard], 128, 0.15, amp=False)
+    q.put((rank, [p.detach().numpy().copy() for p in net.parameters()]))
+    torch.distributed.destroy_process_group()
+
+
+def test_two_rank_ppo_epoch_equals_full_batch():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_epoch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    from bgx.train import ppo_epoch
+    net, opt, sc = _fresh_net()
+    ppo_epoch(net, opt, sc, [_epoch_inputs(256)], 256, 0.15, amp=False)
+    for i, p in enumerate(net.parameters()):
+        assert np.allclose(res[0][i], p.detach().numpy(), atol=1e-5, rtol=1e-4)
+        assert np.allclose(res[1][i], res[0][i])
