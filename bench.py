@@ -50,11 +50,17 @@ def parse():
 def dist_init():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # "nccl" is RCCL on ROCm (one rank per GPU); BGX_DIST_BACKEND=gloo lets
+        # several ranks share one GPU for functional rehearsals of the N>1 path
+        backend = os.environ.get("BGX_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, ws, local
 
 
@@ -276,9 +282,9 @@ def main():
         "dtype": "int8 boards / bf16 policy MLP",
         "data": "synthetic self-play (Philox dice), random-init BackgammonPolicyNetwork weights",
         "burn_in": args.burn_in,
-        "config": {"workload": ("C3: B=65536 games/GPU PPO rollout step (policy 198->128->{500,1} + masked "
+        "config": {"workload": (f"C3: B={B} games/GPU PPO rollout step (policy 198->128->{{500,1}} + masked "
                                 "sample + env.step)") if args.workload == "c3" else
-                   "C1-on-GPU: B=65536 games/GPU random legal policy env.step",
+                   f"C1-on-GPU: B={B} games/GPU random legal policy env.step",
                    "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
                    "parallelism": f"dp{ws} (independent game shards)"},
         "roofline": {"kernel": "k_step<0> (apply + dice + move enumeration + dedup, one wave per game)",

@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libbgx.so")
+# BGX_LIB overrides the library path (A/B experiments between builds)
+LIB_PATH = os.environ.get("BGX_LIB") or os.path.join(_HERE, "libbgx.so")
 
 BGX_OK, BGX_EINVAL, BGX_EDEVICE, BGX_ENOMEM, BGX_EOVERFLOW = 0, -1, -2, -3, -4
 DICE_MT_LANE, DICE_MT_SHARED, DICE_PHILOX = 0, 1, 2

@@ -226,10 +226,14 @@ def main():
     ap.add_argument("--returns", default="lane", choices=["lane", "reference"])
     args = ap.parse_args()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if ws > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("BGX_DIST_BACKEND", "nccl")     # nccl == RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     tr = PPOTrainer(batch=args.batch, horizon=args.horizon, hidden=args.hidden, seed=args.seed,
                     returns=args.returns)
     for u in range(args.updates):

@@ -189,7 +189,10 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, int lane) {
 // 4-long leaves are attempted unconditionally), so all of them are duplicates
 // and the revisit is a no-op: skip it.  Memo tables are per depth (2 and 3),
 // 256 slots each in LDS; when one fills up it stops recording (still exact).
-constexpr int kLogMemo = 8;
+#ifndef BGX_LOG_MEMO
+#define BGX_LOG_MEMO 8
+#endif
+constexpr int kLogMemo = BGX_LOG_MEMO;
 constexpr int kMemoCap = (7 << kLogMemo) / 8;
 
 // Where surviving entries go.  MoveSink: the env's ordered move list in HBM

@@ -163,7 +163,32 @@ struct Args {
     int32_t* err;
     int B, max_moves, dice_mode, auto_reset, match_length;
     uint32_t key0, key1;
+    uint64_t* stamps;         // diagnostics only (env BGX_STAMPS): [B][2] start/end s_memrealtime
+    // dispatch order (Philox mode): each step predicts its lane's next-turn cost class
+    // into cls; k_order turns the classes into perm (heaviest first) for the next launch.
+    int32_t* perm;            // blockIdx -> lane, or null (identity)
+    uint8_t* cls;             // [B] predicted cost class, or null
 };
+
+constexpr int kClasses = 4;
+
+// Cost class of the lane's NEXT movegen (0 = heaviest).  Philox dice are a pure
+// function of (key, lane, counter), so the next roll is known now; the mover
+// after the next apply is 1 - cur.  Doubles dominate (a 4-deep DFS) and grow
+// with the number of points the mover occupies.  Only a scheduling hint.
+__device__ __forceinline__ int predict_class(int bv, uint64_t ctr, const Args& A, int gi) {
+    if (rd(bv, R_OVER)) return kClasses - 1;              // next: reset -> opening roll (never doubles)
+    Rng r;
+    r.init_philox(ctr, A.key0, A.key1, (uint32_t)gi);
+    const int a = r.die(), b = r.die();
+    if (a != b) return kClasses - 1;
+    const int nxt = 1 - rd(bv, R_CUR);
+    const int l = lane_id();
+    const int off = nxt * 24;
+    const bool mine = l >= off && l < off + 24 && bv > 0;
+    const int pts = __popcll(__ballot(mine)) + (rd(bv, 48 + nxt) > 0 ? 2 : 0);
+    return pts >= 8 ? 0 : pts >= 6 ? 1 : 2;
+}
 
 // Enumerate the legal moves of (board in bv, player pl, roll) into `out`.
 // Returns n_moves (truncated); *total = untruncated count; *ovf on overflow.
@@ -192,11 +217,12 @@ __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint6
 // Roll + movegen + obs for one lane according to its `need` byte
 // (reset: backgammon_env.py:78-113; pass/turn: :183-188 roll_dice + update_legal_moves).
 template <int LOG>
-__device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4* lds_tab, uint4* lds_memo) {
+__device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4* lds_tab, uint4* lds_memo,
+                                            uint64_t* ctr_io) {
     const int need = rd(bv, R_NEED);
     if (need == NEED_NONE) return bv;
     Rng rng;
-    if (A.dice_mode == BGX_DICE_PHILOX) rng.init_philox(A.ctr[gi], A.key0, A.key1, (uint32_t)gi);
+    if (A.dice_mode == BGX_DICE_PHILOX) rng.init_philox(*ctr_io, A.key0, A.key1, (uint32_t)gi);
     else if (A.dice_mode == BGX_DICE_MT_LANE) rng.init_mt(A.mt + (size_t)gi * kMtWords, (uint32_t*)lds_tab);
     int r0, r1;
     if (need == NEED_RESET) {
@@ -223,6 +249,7 @@ __device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4
         }
     }
     rng.finish(A.ctr + gi);
+    if (A.dice_mode == BGX_DICE_PHILOX) *ctr_io = rng.ctr;
     bv = wr(bv, R_ROLL0, r0);
     bv = wr(bv, R_ROLL1, r1);
     const int cur = rd(bv, R_CUR);
@@ -329,6 +356,8 @@ struct bgx_engine {
     bg::Args a;
     uint4* slow_tables;
     int slow_waves;
+    int32_t* perm;        // dispatch order for k_step (Philox mode), built by k_order
+    bool perm_valid;
     uint64_t seed;
     // bg_search.hip workspace (grown on demand)
     void* search_ws;

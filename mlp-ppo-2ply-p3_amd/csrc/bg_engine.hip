@@ -32,14 +32,26 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
                                              int32_t* info) {
     __shared__ uint4 tab[1 << LOG];
     __shared__ uint4 memo[2 << kLogMemo];
-    const int gi = blockIdx.x;
+    const int gi = A.perm ? (int)ufl((uint32_t)A.perm[blockIdx.x]) : (int)blockIdx.x;
+    const uint64_t t0 = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    // issue the independent loads together (record, action, dice counter)
     int bv = load_rec(A, gi);
-    if (PHASE != 2) bv = apply_lane(bv, gi, (int)ufl((uint32_t)actions[gi]), A, reward, done, info);
+    const int act = PHASE != 2 ? (int)ufl((uint32_t)actions[gi]) : 0;
+    uint64_t ctr = A.dice_mode == BGX_DICE_PHILOX ? A.ctr[gi] : 0;
+    if (PHASE != 2) bv = apply_lane(bv, gi, act, A, reward, done, info);
     if (PHASE != 1) {
-        bv = advance_lane<LOG>(bv, gi, A, tab, memo);
+        bv = advance_lane<LOG>(bv, gi, A, tab, memo, &ctr);
         if (obs) write_obs(bv, obs + (size_t)gi * 198);
     }
     store_rec(A, gi, bv);
+    if (PHASE == 0 && A.cls) {
+        const int c = predict_class(bv, ctr, A, gi);
+        if (lane_id() == 0) A.cls[gi] = (uint8_t)c;
+    }
+    if (A.stamps && lane_id() == 0) {
+        A.stamps[2 * gi] = t0;
+        A.stamps[2 * gi + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 template <int LOG>
@@ -48,13 +60,66 @@ __global__ __launch_bounds__(64) void k_reset(Args A, const uint8_t* lane_mask, 
     __shared__ uint4 memo[2 << kLogMemo];
     const int gi = blockIdx.x;
     int bv = load_rec(A, gi);
+    uint64_t ctr = A.dice_mode == BGX_DICE_PHILOX ? A.ctr[gi] : 0;
     const bool sel = lane_mask == nullptr || ufl(lane_mask[gi]) != 0u;
     if (sel) bv = wr(bv, R_NEED, NEED_RESET);
     if (!mark_only) {
-        bv = advance_lane<LOG>(bv, gi, A, tab, memo);
+        bv = advance_lane<LOG>(bv, gi, A, tab, memo, &ctr);
         if (obs) write_obs(bv, obs + (size_t)gi * 198);
+        if (A.cls) {
+            const int c = predict_class(bv, ctr, A, gi);
+            if (lane_id() == 0) A.cls[gi] = (uint8_t)c;
+        }
     }
     store_rec(A, gi, bv);
+}
+
+// Counting sort of the predicted classes into the next dispatch order (one
+// workgroup; stable, so the order is deterministic).  perm is always a full
+// permutation of 0..B-1 whatever cls holds.
+__global__ __launch_bounds__(1024) void k_order(const uint8_t* cls, int32_t* perm, int B) {
+    __shared__ int off[kClasses * 1024];
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int chunk = (B + 1023) / 1024;
+    const int lo = min(B, t * chunk), hi = min(B, lo + chunk);
+    int cnt[kClasses];
+    #pragma unroll
+    for (int c = 0; c < kClasses; ++c) cnt[c] = 0;
+    for (int i = lo; i < hi; ++i) {
+        const int c = min((int)cls[i], kClasses - 1);
+        #pragma unroll
+        for (int k = 0; k < kClasses; ++k) cnt[k] += c == k;
+    }
+    // exclusive scan over the class-major array off[c * 1024 + t]
+    #pragma unroll
+    for (int c = 0; c < kClasses; ++c) off[c * 1024 + t] = cnt[c];
+    __syncthreads();
+    int v[kClasses], s = 0;
+    #pragma unroll
+    for (int k = 0; k < kClasses; ++k) { v[k] = off[t * kClasses + k]; s += v[k]; }
+    part[t] = s;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int x = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    int run = part[t] - s;
+    #pragma unroll
+    for (int k = 0; k < kClasses; ++k) { off[t * kClasses + k] = run; run += v[k]; }
+    __syncthreads();
+    int pos[kClasses];
+    #pragma unroll
+    for (int c = 0; c < kClasses; ++c) pos[c] = off[c * 1024 + t];
+    for (int i = lo; i < hi; ++i) {
+        const int c = min((int)cls[i], kClasses - 1);
+        int p = 0;
+        #pragma unroll
+        for (int k = 0; k < kClasses; ++k) if (c == k) p = pos[k]++;
+        perm[p] = i;
+    }
 }
 
 // SHARED dice: one wave draws every lane's dice from ONE MT stream in lane order
@@ -285,6 +350,7 @@ int bgx_internal_fail(hipError_t e) { return fail(e); }
 #define LAUNCH_LOG(e, K, grid, s, ...)                                                            \
     do {                                                                                          \
         if ((e)->lds_log == 9) hipLaunchKernelGGL(K<9>, grid, dim3(64), 0, s, __VA_ARGS__);       \
+        else if ((e)->lds_log == 11) hipLaunchKernelGGL(K<11>, grid, dim3(64), 0, s, __VA_ARGS__); \
         else hipLaunchKernelGGL(K<10>, grid, dim3(64), 0, s, __VA_ARGS__);                        \
     } while (0)
 #define CKL() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return fail(_e); } while (0)
@@ -318,7 +384,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     e->device = device;
     e->seed = seed;
     const char* ll = getenv("BGX_LDS_LOG");
-    e->lds_log = (ll && atoi(ll) == 9) ? 9 : 10;
+    e->lds_log = ll ? atoi(ll) : 10;
+    if (e->lds_log < 9 || e->lds_log > 11) e->lds_log = 10;
     Args& A = e->a;
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
@@ -337,10 +404,16 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     alloc((void**)&A.ovf_queue, 2 * B * 4);
     alloc((void**)&A.err, 16);
     alloc((void**)&e->slow_tables, (size_t)kSlowWaves * ((size_t)16 << kLogSlotsSlow));
+    if (getenv("BGX_STAMPS")) alloc((void**)&A.stamps, B * 16);
+    const char* so = getenv("BGX_ORDER");
+    if (dice_mode == BGX_DICE_PHILOX && !(so && so[0] == '0')) {
+        alloc((void**)&e->perm, B * 4);
+        alloc((void**)&A.cls, B);
+    }
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }
     if (hipMemset(A.lanes, 0, B * 64) != hipSuccess || hipMemset(A.ctr, 0, B * 8) != hipSuccess ||
         hipMemset(A.ovf_count, 0, 16) != hipSuccess || hipMemset(A.err, 0, 16) != hipSuccess ||
-        hipMemset(A.n_total, 0, B * 4) != hipSuccess) {
+        hipMemset(A.n_total, 0, B * 4) != hipSuccess || (A.cls && hipMemset(A.cls, 0, B) != hipSuccess)) {
         bgx_engine_destroy(e);
         return fail(hipGetLastError());
     }
@@ -358,7 +431,7 @@ int bgx_engine_destroy(bgx_engine* e) {
     (void)hipSetDevice(e->device);
     Args& A = e->a;
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
-                    e->slow_tables, e->search_ws};
+                    e->slow_tables, e->search_ws, A.stamps, e->perm, A.cls};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete e;
     return BGX_OK;
@@ -399,6 +472,14 @@ int bgx_engine_mt_state(bgx_engine* e, int32_t lane, uint32_t* state_host, int32
     return BGX_OK;
 }
 
+// diagnostics: copy the per-lane [start, end] s_memrealtime stamps of the last step
+extern "C" int bgx_debug_stamps(bgx_engine* e, uint64_t* host_out) {
+    if (!e || !host_out || !e->a.stamps) return BGX_EINVAL;
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(host_out, e->a.stamps, (size_t)e->a.B * 16, hipMemcpyDeviceToHost));
+    return BGX_OK;
+}
+
 int bgx_engine_buffers(bgx_engine* e, bgx_buffers* out) {
     if (!e || !out) return BGX_EINVAL;
     out->lanes = e->a.lanes; out->moves = e->a.moves; out->n_total = e->a.n_total;
@@ -420,6 +501,10 @@ int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void*
         LAUNCH_LOG(e, k_reset, dim3(A.B), s, A, lane_mask_dev, obs_dev, 0);
     }
     CKL();
+    if (A.cls) {
+        hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, A.cls, e->perm, A.B);
+        e->perm_valid = true;
+    }
     return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
 }
 
@@ -441,12 +526,21 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
             hipLaunchKernelGGL((k_step<2, 10>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev,
                                done_dev, info_dev);
     } else {
+        Args a = A;
+        a.perm = e->perm_valid ? e->perm : nullptr;
         if (e->lds_log == 9)
-            hipLaunchKernelGGL((k_step<0, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
+            hipLaunchKernelGGL((k_step<0, 9>), dim3(A.B), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev, done_dev,
                                info_dev);
-        else
-            hipLaunchKernelGGL((k_step<0, 10>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev,
+        else if (e->lds_log == 11)
+            hipLaunchKernelGGL((k_step<0, 11>), dim3(A.B), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
                                done_dev, info_dev);
+        else
+            hipLaunchKernelGGL((k_step<0, 10>), dim3(A.B), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
+                               done_dev, info_dev);
+        if (A.cls) {
+            hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, A.cls, e->perm, A.B);
+            e->perm_valid = true;
+        }
     }
     CKL();
     return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
