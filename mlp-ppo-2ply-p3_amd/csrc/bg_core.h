@@ -174,6 +174,62 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
 }
 
+// Per-lane lookup that also reports where the key would go: on a miss, `slot`
+// is the first empty slot of the key's probe sequence.
+template <int LOG_SLOTS, typename SlotPtr>
+__device__ __forceinline__ bool probe_lane(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                                           uint32_t& slot) {
+    constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
+    uint32_t h = key_hash(a, b, c, d) & mask;
+    for (;;) {
+        const uint4 v = tab[h];
+        if (v.x == a && v.y == b && v.z == c && v.w == d) { slot = h; return true; }
+        if ((v.x | v.y | v.z | v.w) == 0u) { slot = h; return false; }
+        h = (h + 1u) & mask;
+    }
+}
+
+// Insert the keys of the lanes in `fresh` -- pairwise distinct and all absent,
+// each lane's `slot` from probe_lane against the current table -- in lane
+// order.  A lane whose empty slot was just taken moves on to the next empty
+// slot of its own probe sequence (linear probing stays valid).
+template <int LOG_SLOTS, typename SlotPtr>
+__device__ __forceinline__ void place_absent(SlotPtr tab, uint64_t fresh, uint32_t a, uint32_t b, uint32_t c,
+                                             uint32_t d, uint32_t slot) {
+    constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
+    const int lane = threadIdx.x & 63;
+    while (fresh) {
+        const int src = __ffsll((unsigned long long)fresh) - 1;
+        fresh &= fresh - 1;
+        const uint32_t hs = rdl(slot, src);
+        if (lane == src) tab[hs] = make_uint4(a, b, c, d);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (((fresh >> lane) & 1ull) && slot == hs) {
+            for (;;) {
+                slot = (slot + 1u) & mask;
+                const uint4 v = tab[slot];
+                if ((v.x | v.y | v.z | v.w) == 0u) break;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int lane_rank(uint64_t m) {          // set bits of m below this lane
+    const int lane = threadIdx.x & 63;
+    return __popcll(m & ((1ull << lane) - 1ull));
+}
+
+__device__ __forceinline__ Node rd_node(const Node& t, int src) {
+    Node s;
+    s.lo = (uint64_t)rdl((uint32_t)t.lo, src) | ((uint64_t)rdl((uint32_t)(t.lo >> 32), src) << 32);
+    s.hi = rdl(t.hi, src);
+    s.k3 = rdl(t.k3, src);
+    s.occ = rdl(t.occ, src);
+    s.blot = rdl(t.blot, src);
+    s.n_home = (int)rdl((uint32_t)t.n_home, src);
+    return s;
+}
+
 // ------------------------------------------------------------ enumeration --
 // Filtered-list bookkeeping (filter_full_moves_by_max_submoves,
 // get_all_moves.py:73-94): entries shorter than the running maximum can never
@@ -204,6 +260,11 @@ struct MoveSink {
     __device__ __forceinline__ void push(const Node&, uint64_t enc, int idx) {
         if (idx < cap && (threadIdx.x & 63) == 0) out[idx] = enc;
     }
+    // entries of the lanes in m (lane order) at idx0, idx0+1, ...
+    __device__ __forceinline__ void push_lanes(uint64_t m, const Node&, uint64_t enc, int idx0) {
+        const int idx = idx0 + lane_rank(m);
+        if (((m >> (threadIdx.x & 63)) & 1ull) && idx < cap) out[idx] = enc;
+    }
 };
 
 template <int LOG_SLOTS, typename SlotPtr, typename Sink = MoveSink>
@@ -229,103 +290,149 @@ struct Gen {
         }
     }
 
-    // All children of node s (list k, die d) as entries prefix | enc << shift of
-    // length len, in child order.  Children of one node are pairwise distinct
-    // afterstates (different source points), so their duplicate checks against
-    // the set as it stood before the batch run one child per lane; only the new
-    // ones are then inserted, serially and in child order -- the same set, list
-    // order and counts as the reference's one-by-one add_unique_board calls.
-    __device__ __forceinline__ void leaf_batch(const Node& s, const Kids& k, int d, uint64_t prefix, int shift,
-                                               int len) {
+    // Child `lane` of node s (list k, die d) on each lane whose bit is set in
+    // k.bits: the expansion of one node runs one child per lane.
+    __device__ __forceinline__ bool lane_child(const Node& s, const Kids& k, int d, Node& t, uint32_t& enc) const {
         const int l = threadIdx.x & 63;
         const bool act = l < 32 && ((k.bits >> l) & 1u);
-        uint32_t ka = 0, kb = 0, kc = 0, kd = 0, ke = 0;
-        bool fresh = false;
         if (act) {
             const Sub m = child(s, k, l, d, pl);
-            const Node t = apply(s, m, pl);
-            ka = (uint32_t)t.lo; kb = (uint32_t)(t.lo >> 32); kc = t.hi; kd = t.k3; ke = m.enc;
-            fresh = !table_contains_lane<LOG_SLOTS>(tab, ka, kb, kc, kd);
+            t = apply(s, m, pl);
+            enc = m.enc;
         }
-        uint64_t nm = __ballot(fresh);
-        while (nm) {
-            const int src = __ffsll((unsigned long long)nm) - 1;
-            nm &= nm - 1;
-            Node t;
-            t.lo = (uint64_t)rdl(ka, src) | ((uint64_t)rdl(kb, src) << 32);
-            t.hi = rdl(kc, src);
-            t.k3 = rdl(kd, src);
-            const uint32_t enc = rdl(ke, src);
-            table_insert<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3);
-            if (++n_unique >= cap_unique) { ovf = true; return; }
-            if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
-            if (len == cur_max) {
-                sink.push(t, prefix | ((uint64_t)enc << shift), count);
-                ++count;
-            }
+        return act;
+    }
+
+    // Add the entries of the lanes in `fresh` (length len), in lane order.
+    __device__ __forceinline__ void commit(uint64_t fresh, const Node& t, uint64_t enc, uint32_t slot, int len) {
+        const int n = __popcll(fresh);
+        if (!n) return;
+        if (n_unique + n >= cap_unique) { ovf = true; return; }
+        place_absent<LOG_SLOTS>(tab, fresh, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        n_unique += n;
+        if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
+        if (len == cur_max) {
+            sink.push_lanes(fresh, t, enc, count);
+            count += n;
         }
     }
 
-    // handle_non_doubles (handle_moves.py:109-200)
+    // Siblings (children of one node) are pairwise distinct afterstates
+    // (different source points), so their duplicate checks against the set as
+    // it stood before the batch run one per lane and only the new ones are
+    // added, in child order -- the same set, list order and counts as the
+    // reference's one-by-one add_unique_board calls.
+    __device__ __forceinline__ void batch(bool act, const Node& t, uint64_t enc, int len) {
+        uint32_t slot = 0;
+        bool found = true;
+        if (act) found = probe_lane<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        commit(__ballot(act && !found), t, enc, slot, len);
+    }
+
+    // All children of s as entries prefix | enc << shift of length len.
+    __device__ __forceinline__ void leaf_batch(const Node& s, const Kids& k, int d, uint64_t prefix, int shift,
+                                               int len) {
+        Node t;
+        uint32_t e = 0;
+        const bool act = lane_child(s, k, d, t, e);
+        batch(act, t, prefix | ((uint64_t)e << shift), len);
+    }
+
+    // handle_non_doubles (handle_moves.py:109-200); the pre-scan (:144-155) is
+    // one ballot over the lane-parallel first level.
     __device__ __forceinline__ void pass_nd(const Node& s0, int da, int db) {
         const Kids k1 = gen(s0, da, pl, blocked);
-        bool exists = false;
-        for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {          // pre-scan (:144-155)
-            const Sub m1 = child(s0, k1, __builtin_ctz(b1), da, pl);
-            const Node s1 = apply(s0, m1, pl);
-            if (gen(s1, db, pl, blocked).bits) { exists = true; break; }
+        Node t1;
+        uint32_t e1 = 0;
+        const bool a1 = lane_child(s0, k1, da, t1, e1);
+        uint32_t q2 = 0;
+        int x2 = -1;
+        if (a1) { const Kids k = gen(t1, db, pl, blocked); q2 = k.bits; x2 = k.extra; }
+        if (__ballot(a1 && q2 != 0u) == 0ull) {       // no two-dice sequence: the singles
+            batch(a1, t1, (uint64_t)e1, 1);
+            return;
         }
         for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
-            const Sub m1 = child(s0, k1, __builtin_ctz(b1), da, pl);
-            const Node s1 = apply(s0, m1, pl);
-            if (exists) {
-                const Kids k2 = gen(s1, db, pl, blocked);
-                if (k2.bits) { leaf_batch(s1, k2, db, (uint64_t)m1.enc, 16, 2); if (ovf) return; }
-            } else {
-                insert(s1, (uint64_t)m1.enc, 1);
-                if (ovf) return;
-            }
+            const int i = __builtin_ctz(b1);
+            const Kids k2{rdl(q2, i), (int)rdl((uint32_t)x2, i)};
+            if (!k2.bits) continue;
+            leaf_batch(rd_node(t1, i), k2, db, (uint64_t)rdl(e1, i), 16, 2);
+            if (ovf) return;
         }
     }
 
-    // true if (s, depth) was seen before (=> skip); records it otherwise
-    __device__ __forceinline__ bool seen(const Node& s, uint4* memo, int& nm) {
-        if (!memo) return false;
-        const bool fresh = table_insert<kLogMemo>(memo, (uint32_t)s.lo, (uint32_t)(s.lo >> 32), s.hi, s.k3,
-                                                  nm < kMemoCap);
-        if (fresh && nm < kMemoCap) ++nm;
-        return !fresh;
+    // Revisit check of a sibling batch at one depth: returns the lanes not seen
+    // before and records them (while the memo has room).
+    __device__ __forceinline__ uint64_t memo_batch(uint4* memo, int& nm, bool act, const Node& t) {
+        if (!memo) return __ballot(act);
+        uint32_t slot = 0;
+        bool found = true;
+        if (act) found = probe_lane<kLogMemo>(memo, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        const uint64_t fresh = __ballot(act && !found);
+        uint64_t rec = fresh;
+        int n = __popcll(rec);
+        while (n > kMemoCap - nm) { rec &= ~(1ull << (63 - __clzll((long long)rec))); --n; }
+        if (rec) place_absent<kLogMemo>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        nm += n;
+        return fresh;
     }
 
     // handle_doubles (handle_moves.py:203-310): 4-deep pre-order DFS; partial
     // prefixes are inserted at dead ends only until the first 4-long sequence.
+    // Each node's children are expanded one per lane (state, revisit check,
+    // next-level child list); the walk itself stays in order.
     __device__ __forceinline__ void doubles(const Node& s0, int d) {
         bool got4 = false;
         const Kids k1 = gen(s0, d, pl, blocked);
+        Node t1;
+        uint32_t e1 = 0;
+        const bool a1 = lane_child(s0, k1, d, t1, e1);
+        uint32_t q2 = 0;
+        int x2 = -1;
+        if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; x2 = k.extra; }
         for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
-            const Sub m1 = child(s0, k1, __builtin_ctz(b1), d, pl);
-            const Node s1 = apply(s0, m1, pl);
-            const Kids k2 = gen(s1, d, pl, blocked);
-            if (!k2.bits && !got4) { insert(s1, m1.enc, 1); if (ovf) return; }
-            for (uint32_t b2 = k2.bits; b2; b2 &= b2 - 1u) {
-                const Sub m2 = child(s1, k2, __builtin_ctz(b2), d, pl);
-                const Node s2 = apply(s1, m2, pl);
-                if (seen(s2, memo2, n_memo2)) continue;
-                const uint64_t e2 = (uint64_t)m1.enc | ((uint64_t)m2.enc << 16);
-                const Kids k3 = gen(s2, d, pl, blocked);
-                if (!k3.bits && !got4) { insert(s2, e2, 2); if (ovf) return; }
-                for (uint32_t b3 = k3.bits; b3; b3 &= b3 - 1u) {
-                    const Sub m3 = child(s2, k3, __builtin_ctz(b3), d, pl);
-                    const Node s3 = apply(s2, m3, pl);
-                    if (seen(s3, memo3, n_memo3)) continue;
-                    const uint64_t e3 = e2 | ((uint64_t)m3.enc << 32);
-                    const Kids k4 = gen(s3, d, pl, blocked);
-                    if (!k4.bits && !got4) { insert(s3, e3, 3); if (ovf) return; }
-                    if (k4.bits) {
-                        leaf_batch(s3, k4, d, e3, 48, 4);
-                        if (ovf) return;
-                        got4 = true;
+            const int i1 = __builtin_ctz(b1);
+            const Node s1 = rd_node(t1, i1);
+            const Kids k2{rdl(q2, i1), (int)rdl((uint32_t)x2, i1)};
+            const uint64_t m1 = rdl(e1, i1);
+            if (!k2.bits) {
+                if (!got4) { insert(s1, m1, 1); if (ovf) return; }
+                continue;
+            }
+            Node t2;
+            uint32_t e2l = 0;
+            const bool a2 = lane_child(s1, k2, d, t2, e2l);
+            const uint64_t f2 = memo_batch(memo2, n_memo2, a2, t2);
+            uint32_t q3 = 0;
+            int x3 = -1;
+            if ((f2 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; x3 = k.extra; }
+            for (uint64_t b2 = f2; b2; b2 &= b2 - 1ull) {
+                const int i2 = __ffsll((unsigned long long)b2) - 1;
+                const Node s2 = rd_node(t2, i2);
+                const Kids k3{rdl(q3, i2), (int)rdl((uint32_t)x3, i2)};
+                const uint64_t m2 = m1 | ((uint64_t)rdl(e2l, i2) << 16);
+                if (!k3.bits) {
+                    if (!got4) { insert(s2, m2, 2); if (ovf) return; }
+                    continue;
+                }
+                Node t3;
+                uint32_t e3l = 0;
+                const bool a3 = lane_child(s2, k3, d, t3, e3l);
+                const uint64_t f3 = memo_batch(memo3, n_memo3, a3, t3);
+                uint32_t q4 = 0;
+                int x4 = -1;
+                if ((f3 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; x4 = k.extra; }
+                for (uint64_t b3 = f3; b3; b3 &= b3 - 1ull) {
+                    const int i3 = __ffsll((unsigned long long)b3) - 1;
+                    const Kids k4{rdl(q4, i3), (int)rdl((uint32_t)x4, i3)};
+                    const uint64_t m3 = m2 | ((uint64_t)rdl(e3l, i3) << 32);
+                    if (!k4.bits) {
+                        if (!got4) { insert(rd_node(t3, i3), m3, 3); if (ovf) return; }
+                        continue;
                     }
+                    leaf_batch(rd_node(t3, i3), k4, d, m3, 48, 4);
+                    if (ovf) return;
+                    got4 = true;
                 }
             }
         }

@@ -358,6 +358,8 @@ struct bgx_engine {
     int slow_waves;
     int32_t* perm;        // dispatch order for k_step (Philox mode), built by k_order
     bool perm_valid;
+    hipStream_t side;     // light launch of the split step
+    hipEvent_t ev_fork, ev_join;
     uint64_t seed;
     // bg_search.hip workspace (grown on demand)
     void* search_ws;

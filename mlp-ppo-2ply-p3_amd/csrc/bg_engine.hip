@@ -14,6 +14,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -27,12 +28,17 @@ using namespace bg;
 
 // -------------------------------------------------------------- kernels --
 // PHASE 0: apply + advance fused (per-lane dice); 1: apply only; 2: advance only.
-template <int PHASE, int LOG>
+// `base` offsets blockIdx into the dispatch order; MEMO=false drops the doubles
+// memo tables (8 KB of LDS) for the light launch -- still exact, only slower on
+// an (unpredicted) doubles lane.
+template <int PHASE, int LOG, bool MEMO = true>
 __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
-                                             int32_t* info) {
+                                             int32_t* info, int base) {
     __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo[2 << kLogMemo];
-    const int gi = A.perm ? (int)ufl((uint32_t)A.perm[blockIdx.x]) : (int)blockIdx.x;
+    __shared__ uint4 memo_[MEMO ? (2 << kLogMemo) : 1];
+    uint4* memo = MEMO ? memo_ : nullptr;
+    const int bi = (int)blockIdx.x + base;
+    const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : bi;
     const uint64_t t0 = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     // issue the independent loads together (record, action, dice counter)
     int bv = load_rec(A, gi);
@@ -355,6 +361,14 @@ int bgx_internal_fail(hipError_t e) { return fail(e); }
     } while (0)
 #define CKL() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return fail(_e); } while (0)
 
+// Launch size of the heavy (doubles) share: the expected doubles fraction 1/6 plus
+// 4 sigma; lanes past it run in the light launch whatever their class.
+static int heavy_grid(int B) {
+    const char* f = getenv("BGX_HEAVY_FRAC");
+    double g = f ? atof(f) * B : B / 6.0 + 4.0 * std::sqrt(B * 5.0 / 36.0) + 32.0;
+    return g >= B ? B : (int)g;
+}
+
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
                      const uint8_t* dice, int cap, int16_t* nm, int32_t* nt, uint64_t* moves) {
     if (src == 0) {
@@ -409,6 +423,9 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     if (dice_mode == BGX_DICE_PHILOX && !(so && so[0] == '0')) {
         alloc((void**)&e->perm, B * 4);
         alloc((void**)&A.cls, B);
+        if (err == hipSuccess) err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
+        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
     }
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }
     if (hipMemset(A.lanes, 0, B * 64) != hipSuccess || hipMemset(A.ctr, 0, B * 8) != hipSuccess ||
@@ -433,6 +450,9 @@ int bgx_engine_destroy(bgx_engine* e) {
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
                     e->slow_tables, e->search_ws, A.stamps, e->perm, A.cls};
     for (void* p : ptrs) if (p) (void)hipFree(p);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->side) (void)hipStreamDestroy(e->side);
     delete e;
     return BGX_OK;
 }
@@ -517,26 +537,40 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
     if (A.dice_mode == BGX_DICE_MT_SHARED) {
         hipLaunchKernelGGL((k_step<1, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
-                           info_dev);
+                           info_dev, 0);
         hipLaunchKernelGGL(k_shared_dice, dim3(1), dim3(64), 0, s, A);
         if (e->lds_log == 9)
             hipLaunchKernelGGL((k_step<2, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
-                               info_dev);
+                               info_dev, 0);
         else
             hipLaunchKernelGGL((k_step<2, 10>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev,
-                               done_dev, info_dev);
+                               done_dev, info_dev, 0);
     } else {
         Args a = A;
         a.perm = e->perm_valid ? e->perm : nullptr;
+        // split dispatch (Philox mode): the predicted-doubles prefix of the order on
+        // the caller's stream with the big table + memo, the rest concurrently on a
+        // side stream with a small table (8 KB of LDS -> ~3x the resident waves)
+        const int heavy = a.perm ? heavy_grid(A.B) : A.B;
+        if (heavy < A.B) {
+            CK(hipEventRecord(e->ev_fork, s));
+            CK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+            hipLaunchKernelGGL((k_step<0, 9, false>), dim3(A.B - heavy), dim3(64), 0, e->side, a, actions_dev, obs_dev,
+                               reward_dev, done_dev, info_dev, heavy);
+        }
         if (e->lds_log == 9)
-            hipLaunchKernelGGL((k_step<0, 9>), dim3(A.B), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev, done_dev,
-                               info_dev);
+            hipLaunchKernelGGL((k_step<0, 9>), dim3(heavy), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev, done_dev,
+                               info_dev, 0);
         else if (e->lds_log == 11)
-            hipLaunchKernelGGL((k_step<0, 11>), dim3(A.B), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
-                               done_dev, info_dev);
+            hipLaunchKernelGGL((k_step<0, 11>), dim3(heavy), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
+                               done_dev, info_dev, 0);
         else
-            hipLaunchKernelGGL((k_step<0, 10>), dim3(A.B), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
-                               done_dev, info_dev);
+            hipLaunchKernelGGL((k_step<0, 10>), dim3(heavy), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
+                               done_dev, info_dev, 0);
+        if (heavy < A.B) {
+            CK(hipEventRecord(e->ev_join, e->side));
+            CK(hipStreamWaitEvent(s, e->ev_join, 0));
+        }
         if (A.cls) {
             hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, A.cls, e->perm, A.B);
             e->perm_valid = true;

@@ -129,6 +129,21 @@ struct MinSink {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         if (slot == kKeyCap - 1) flush(kKeyCap);
     }
+
+    // keys of the lanes in m (<= 32 of them), list positions idx0, idx0+1, ...
+    __device__ __forceinline__ void push_lanes(uint64_t m, const Node& t, uint64_t, int idx0) {
+        const int pos = idx0 % kKeyCap, n = __popcll(m);
+        const int r = lane_rank(m);
+        const bool on = (m >> (threadIdx.x & 63)) & 1ull;
+        const uint4 key = make_uint4((uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3);
+        if (on && pos + r < kKeyCap) klist[pos + r] = key;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        if (pos + n >= kKeyCap) {
+            flush(kKeyCap);
+            if (on && pos + r >= kKeyCap) klist[pos + r - kKeyCap] = key;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        }
+    }
 };
 
 __device__ __forceinline__ uint64_t uload64(const uint64_t* p) {
