@@ -267,7 +267,13 @@ struct MoveSink {
     }
 };
 
-template <int LOG_SLOTS, typename SlotPtr, typename Sink = MoveSink>
+// TAGGED: the revisit memo lives in the dedup table itself under tagged keys
+// (hit-mask field complemented: >= 20 bits set, impossible for a real
+// afterstate, which hits at most 4 blots; depth 3 also flips the bar nibble,
+// and bar + off + sum(counts) = 15 keeps the depth-2 and depth-3 images apart).
+constexpr uint32_t kTag2 = 0xFFFFFF00u, kTag3 = 0xFFFFFF0Fu;
+
+template <int LOG_SLOTS, typename SlotPtr, typename Sink = MoveSink, bool TAGGED = false>
 struct Gen {
     SlotPtr tab;
     uint4* memo2;       // LDS memo tables (nullptr = no pruning)
@@ -279,10 +285,14 @@ struct Gen {
     int cur_max, count, n_unique, cap_unique;
     bool ovf;
 
+    // table slots in use (dedup entries + tagged memo entries)
+    __device__ __forceinline__ int fill() const { return n_unique + (TAGGED ? n_memo2 + n_memo3 : 0); }
+
     __device__ __forceinline__ void insert(const Node& s, uint64_t enc, int len) {
         const uint32_t a = (uint32_t)s.lo, b = (uint32_t)(s.lo >> 32);
         if (!table_insert<LOG_SLOTS>(tab, a, b, s.hi, s.k3)) return;
-        if (++n_unique >= cap_unique) { ovf = true; return; }
+        ++n_unique;
+        if (fill() >= cap_unique) { ovf = true; return; }
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
             sink.push(s, enc, count);
@@ -307,7 +317,7 @@ struct Gen {
     __device__ __forceinline__ void commit(uint64_t fresh, const Node& t, uint64_t enc, uint32_t slot, int len) {
         const int n = __popcll(fresh);
         if (!n) return;
-        if (n_unique + n >= cap_unique) { ovf = true; return; }
+        if (fill() + n >= cap_unique) { ovf = true; return; }
         place_absent<LOG_SLOTS>(tab, fresh, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
         n_unique += n;
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
@@ -363,16 +373,25 @@ struct Gen {
 
     // Revisit check of a sibling batch at one depth: returns the lanes not seen
     // before and records them (while the memo has room).
-    __device__ __forceinline__ uint64_t memo_batch(uint4* memo, int& nm, bool act, const Node& t) {
+    __device__ __forceinline__ uint64_t memo_batch(uint4* memo, int& nm, bool act, const Node& t, uint32_t tag) {
         if (!memo) return __ballot(act);
         uint32_t slot = 0;
         bool found = true;
-        if (act) found = probe_lane<kLogMemo>(memo, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        const uint32_t k3 = TAGGED ? t.k3 ^ tag : t.k3;
+        if (act) {
+            if (TAGGED) found = probe_lane<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            else found = probe_lane<kLogMemo>(memo, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+        }
         const uint64_t fresh = __ballot(act && !found);
         uint64_t rec = fresh;
         int n = __popcll(rec);
-        while (n > kMemoCap - nm) { rec &= ~(1ull << (63 - __clzll((long long)rec))); --n; }
-        if (rec) place_absent<kLogMemo>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        int room = kMemoCap - nm;
+        if (TAGGED) room = min(room, cap_unique / 3 - n_memo2 - n_memo3);
+        while (n > room && rec) { rec &= ~(1ull << (63 - __clzll((long long)rec))); --n; }
+        if (rec) {
+            if (TAGGED) place_absent<LOG_SLOTS>(tab, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            else place_absent<kLogMemo>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+        }
         nm += n;
         return fresh;
     }
@@ -402,7 +421,7 @@ struct Gen {
             Node t2;
             uint32_t e2l = 0;
             const bool a2 = lane_child(s1, k2, d, t2, e2l);
-            const uint64_t f2 = memo_batch(memo2, n_memo2, a2, t2);
+            const uint64_t f2 = memo_batch(memo2, n_memo2, a2, t2, kTag2);
             uint32_t q3 = 0;
             int x3 = -1;
             if ((f2 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; x3 = k.extra; }
@@ -418,7 +437,7 @@ struct Gen {
                 Node t3;
                 uint32_t e3l = 0;
                 const bool a3 = lane_child(s2, k3, d, t3, e3l);
-                const uint64_t f3 = memo_batch(memo3, n_memo3, a3, t3);
+                const uint64_t f3 = memo_batch(memo3, n_memo3, a3, t3, kTag3);
                 uint32_t q4 = 0;
                 int x4 = -1;
                 if ((f3 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; x4 = k.extra; }

@@ -192,19 +192,19 @@ __device__ __forceinline__ int predict_class(int bv, uint64_t ctr, const Args& A
 
 // Enumerate the legal moves of (board in bv, player pl, roll) into `out`.
 // Returns n_moves (truncated); *total = untruncated count; *ovf on overflow.
-template <int LOG, typename SlotPtr>
+template <int LOG, typename SlotPtr, bool TAGGED = false>
 __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint64_t* out, int cap, SlotPtr tab,
                                            int cap_unique, int* total, bool* ovf, uint4* memo) {
     constexpr int slots = 1 << LOG;
     for (int i = lane_id(); i < slots; i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = r0 == r1;
-    if (memo && dbl)
+    if (memo && dbl && !TAGGED)
         for (int i = lane_id(); i < (2 << kLogMemo); i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    Gen<LOG, SlotPtr> g;
+    Gen<LOG, SlotPtr, MoveSink, TAGGED> g;
     g.tab = tab; g.sink.out = out; g.sink.cap = cap; g.pl = pl; g.cap_unique = cap_unique;
     g.memo2 = memo && dbl ? memo : nullptr;
-    g.memo3 = memo && dbl ? memo + (1 << kLogMemo) : nullptr;
+    g.memo3 = memo && dbl ? (TAGGED ? memo : memo + (1 << kLogMemo)) : nullptr;
     uint32_t blocked;
     const Node s0 = node_from_bytes(bv, pl, blocked);
     g.blocked = blocked;
@@ -216,7 +216,7 @@ __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint6
 
 // Roll + movegen + obs for one lane according to its `need` byte
 // (reset: backgammon_env.py:78-113; pass/turn: :183-188 roll_dice + update_legal_moves).
-template <int LOG>
+template <int LOG, bool TAGGED = false>
 __device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4* lds_tab, uint4* lds_memo,
                                             uint64_t* ctr_io) {
     const int need = rd(bv, R_NEED);
@@ -255,7 +255,7 @@ __device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4
     const int cur = rd(bv, R_CUR);
     int total;
     bool ovf;
-    int n = run_movegen<LOG>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves, A.max_moves, lds_tab,
+    int n = run_movegen<LOG, uint4*, TAGGED>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves, A.max_moves, lds_tab,
                              cap_fast<LOG>(), &total, &ovf, lds_memo);
     int flags = rd(bv, R_FLAGS) & ~1;
     if (ovf) {
@@ -352,14 +352,14 @@ __device__ __forceinline__ void store_rec(const Args& A, int gi, int bv) { A.lan
 // Engine object behind the C ABI's opaque bgx_engine*.
 struct bgx_engine {
     int device;
-    int lds_log;      // 9 or 10
+    int lds_log;      // 9, 10 or 11
+    int memo_mode;    // 1: separate memo tables, 2: memo inside the dedup table
     bg::Args a;
     uint4* slow_tables;
     int slow_waves;
     int32_t* perm;        // dispatch order for k_step (Philox mode), built by k_order
     bool perm_valid;
-    hipStream_t side;     // light launch of the split step
-    hipEvent_t ev_fork, ev_join;
+    int32_t* order_cnt;   // k_order_count -> k_order_scatter, [B/1024+1][kClasses]
     uint64_t seed;
     // bg_search.hip workspace (grown on demand)
     void* search_ws;

@@ -14,7 +14,6 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
-#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -28,15 +27,15 @@ using namespace bg;
 
 // -------------------------------------------------------------- kernels --
 // PHASE 0: apply + advance fused (per-lane dice); 1: apply only; 2: advance only.
-// `base` offsets blockIdx into the dispatch order; MEMO=false drops the doubles
-// memo tables (8 KB of LDS) for the light launch -- still exact, only slower on
-// an (unpredicted) doubles lane.
-template <int PHASE, int LOG, bool MEMO = true>
+// `base` offsets blockIdx into the dispatch order.  MEMO: 0 = no revisit memo,
+// 1 = separate memo tables (8 KB of LDS), 2 = memo inside the dedup table
+// (tagged keys; 16 KB per wave in all).
+template <int PHASE, int LOG, int MEMO = 1>
 __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
                                              int32_t* info, int base) {
     __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo_[MEMO ? (2 << kLogMemo) : 1];
-    uint4* memo = MEMO ? memo_ : nullptr;
+    __shared__ uint4 memo_[MEMO == 1 ? (2 << kLogMemo) : 1];
+    uint4* memo = MEMO == 1 ? memo_ : MEMO == 2 ? tab : nullptr;
     const int bi = (int)blockIdx.x + base;
     const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : bi;
     const uint64_t t0 = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -46,7 +45,7 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
     uint64_t ctr = A.dice_mode == BGX_DICE_PHILOX ? A.ctr[gi] : 0;
     if (PHASE != 2) bv = apply_lane(bv, gi, act, A, reward, done, info);
     if (PHASE != 1) {
-        bv = advance_lane<LOG>(bv, gi, A, tab, memo, &ctr);
+        bv = advance_lane<LOG, MEMO == 2>(bv, gi, A, tab, memo, &ctr);
         if (obs) write_obs(bv, obs + (size_t)gi * 198);
     }
     store_rec(A, gi, bv);
@@ -80,51 +79,68 @@ __global__ __launch_bounds__(64) void k_reset(Args A, const uint8_t* lane_mask, 
     store_rec(A, gi, bv);
 }
 
-// Counting sort of the predicted classes into the next dispatch order (one
-// workgroup; stable, so the order is deterministic).  perm is always a full
-// permutation of 0..B-1 whatever cls holds.
-__global__ __launch_bounds__(1024) void k_order(const uint8_t* cls, int32_t* perm, int B) {
-    __shared__ int off[kClasses * 1024];
-    __shared__ int part[1024];
-    const int t = threadIdx.x;
-    const int chunk = (B + 1023) / 1024;
-    const int lo = min(B, t * chunk), hi = min(B, lo + chunk);
-    int cnt[kClasses];
+// Next dispatch order = lanes grouped by predicted class (class 0 first), in
+// lane order within a class: a two-pass counting sort over blocks of 1024
+// lanes.  perm is a full permutation of 0..B-1 whatever cls holds.
+__device__ __forceinline__ int order_class(const uint8_t* cls, int i, int B) {
+    return i < B ? min((int)cls[i], kClasses - 1) : kClasses;     // kClasses = padding, never written
+}
+
+// pass 1: cnt[b][c] = lanes of class c in block b
+__global__ __launch_bounds__(1024) void k_order_count(const uint8_t* cls, int32_t* cnt, int B) {
+    __shared__ int sc[kClasses];
+    const int t = threadIdx.x, i = blockIdx.x * 1024 + t;
+    if (t < kClasses) sc[t] = 0;
+    __syncthreads();
+    const int c = order_class(cls, i, B);
     #pragma unroll
-    for (int c = 0; c < kClasses; ++c) cnt[c] = 0;
-    for (int i = lo; i < hi; ++i) {
-        const int c = min((int)cls[i], kClasses - 1);
-        #pragma unroll
-        for (int k = 0; k < kClasses; ++k) cnt[k] += c == k;
+    for (int k = 0; k < kClasses; ++k) {
+        const uint64_t m = __ballot(c == k);
+        if ((t & 63) == 0 && m) atomicAdd(&sc[k], __popcll(m));
     }
-    // exclusive scan over the class-major array off[c * 1024 + t]
-    #pragma unroll
-    for (int c = 0; c < kClasses; ++c) off[c * 1024 + t] = cnt[c];
     __syncthreads();
-    int v[kClasses], s = 0;
-    #pragma unroll
-    for (int k = 0; k < kClasses; ++k) { v[k] = off[t * kClasses + k]; s += v[k]; }
-    part[t] = s;
+    if (t < kClasses) cnt[blockIdx.x * kClasses + t] = sc[t];
+}
+
+// pass 2: position = (lanes of lower classes) + (class-c lanes of earlier blocks)
+// + (class-c lanes earlier in this block)
+__global__ __launch_bounds__(1024) void k_order_scatter(const uint8_t* cls, const int32_t* cnt, int32_t* perm, int B,
+                                                        int nblk) {
+    __shared__ int tot[kClasses], pre[kClasses], wsum[16][kClasses];
+    const int t = threadIdx.x, b = blockIdx.x, w = t >> 6, l = t & 63;
+    if (t < kClasses) { tot[t] = 0; pre[t] = 0; }
     __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int x = t >= d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
-    }
-    int run = part[t] - s;
+    int a_tot[kClasses], a_pre[kClasses];
     #pragma unroll
-    for (int k = 0; k < kClasses; ++k) { off[t * kClasses + k] = run; run += v[k]; }
-    __syncthreads();
-    int pos[kClasses];
-    #pragma unroll
-    for (int c = 0; c < kClasses; ++c) pos[c] = off[c * 1024 + t];
-    for (int i = lo; i < hi; ++i) {
-        const int c = min((int)cls[i], kClasses - 1);
-        int p = 0;
+    for (int k = 0; k < kClasses; ++k) { a_tot[k] = 0; a_pre[k] = 0; }
+    for (int j = t; j < nblk; j += 1024) {
         #pragma unroll
-        for (int k = 0; k < kClasses; ++k) if (c == k) p = pos[k]++;
-        perm[p] = i;
+        for (int k = 0; k < kClasses; ++k) {
+            const int v = cnt[j * kClasses + k];
+            a_tot[k] += v;
+            a_pre[k] += j < b ? v : 0;
+        }
+    }
+    #pragma unroll
+    for (int k = 0; k < kClasses; ++k) {
+        if (a_tot[k]) atomicAdd(&tot[k], a_tot[k]);
+        if (a_pre[k]) atomicAdd(&pre[k], a_pre[k]);
+    }
+    const int i = b * 1024 + t;
+    const int c = order_class(cls, i, B);
+    int rank = 0;
+    #pragma unroll
+    for (int k = 0; k < kClasses; ++k) {
+        const uint64_t m = __ballot(c == k);
+        if (c == k) rank = __popcll(m & ((1ull << l) - 1ull));
+        if (l == 0) wsum[w][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (c < kClasses) {
+        int pos = pre[c] + rank;
+        for (int k = 0; k < c; ++k) pos += tot[k];
+        for (int v = 0; v < w; ++v) pos += wsum[v][c];
+        perm[pos] = i;
     }
 }
 
@@ -361,12 +377,26 @@ int bgx_internal_fail(hipError_t e) { return fail(e); }
     } while (0)
 #define CKL() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return fail(_e); } while (0)
 
-// Launch size of the heavy (doubles) share: the expected doubles fraction 1/6 plus
-// 4 sigma; lanes past it run in the light launch whatever their class.
-static int heavy_grid(int B) {
-    const char* f = getenv("BGX_HEAVY_FRAC");
-    double g = f ? atof(f) * B : B / 6.0 + 4.0 * std::sqrt(B * 5.0 / 36.0) + 32.0;
-    return g >= B ? B : (int)g;
+static void launch_order(bgx_engine* e, hipStream_t s) {
+    const int nblk = (e->a.B + 1023) / 1024;
+    hipLaunchKernelGGL(k_order_count, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->a.B);
+    hipLaunchKernelGGL(k_order_scatter, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->perm, e->a.B, nblk);
+    e->perm_valid = true;
+}
+
+static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, const int32_t* actions, float* obs,
+                        float* reward, uint8_t* done, int32_t* info) {
+    if (e->memo_mode == 2) {
+        if (e->lds_log == 11)
+            hipLaunchKernelGGL((k_step<0, 11, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+        else
+            hipLaunchKernelGGL((k_step<0, 10, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+    } else if (e->lds_log == 9)
+        hipLaunchKernelGGL((k_step<0, 9>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+    else if (e->lds_log == 11)
+        hipLaunchKernelGGL((k_step<0, 11>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+    else
+        hipLaunchKernelGGL((k_step<0, 10>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
 }
 
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
@@ -400,6 +430,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     const char* ll = getenv("BGX_LDS_LOG");
     e->lds_log = ll ? atoi(ll) : 10;
     if (e->lds_log < 9 || e->lds_log > 11) e->lds_log = 10;
+    const char* mm = getenv("BGX_MEMO_MODE");
+    e->memo_mode = mm ? atoi(mm) : 1;
     Args& A = e->a;
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
@@ -423,9 +455,7 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     if (dice_mode == BGX_DICE_PHILOX && !(so && so[0] == '0')) {
         alloc((void**)&e->perm, B * 4);
         alloc((void**)&A.cls, B);
-        if (err == hipSuccess) err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
-        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
-        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
+        alloc((void**)&e->order_cnt, (B / 1024 + 1) * kClasses * 4);
     }
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }
     if (hipMemset(A.lanes, 0, B * 64) != hipSuccess || hipMemset(A.ctr, 0, B * 8) != hipSuccess ||
@@ -448,11 +478,8 @@ int bgx_engine_destroy(bgx_engine* e) {
     (void)hipSetDevice(e->device);
     Args& A = e->a;
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
-                    e->slow_tables, e->search_ws, A.stamps, e->perm, A.cls};
+                    e->slow_tables, e->search_ws, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
-    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-    if (e->side) (void)hipStreamDestroy(e->side);
     delete e;
     return BGX_OK;
 }
@@ -522,8 +549,7 @@ int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void*
     }
     CKL();
     if (A.cls) {
-        hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, A.cls, e->perm, A.B);
-        e->perm_valid = true;
+        launch_order(e, s);
     }
     return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
 }
@@ -548,33 +574,8 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     } else {
         Args a = A;
         a.perm = e->perm_valid ? e->perm : nullptr;
-        // split dispatch (Philox mode): the predicted-doubles prefix of the order on
-        // the caller's stream with the big table + memo, the rest concurrently on a
-        // side stream with a small table (8 KB of LDS -> ~3x the resident waves)
-        const int heavy = a.perm ? heavy_grid(A.B) : A.B;
-        if (heavy < A.B) {
-            CK(hipEventRecord(e->ev_fork, s));
-            CK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
-            hipLaunchKernelGGL((k_step<0, 9, false>), dim3(A.B - heavy), dim3(64), 0, e->side, a, actions_dev, obs_dev,
-                               reward_dev, done_dev, info_dev, heavy);
-        }
-        if (e->lds_log == 9)
-            hipLaunchKernelGGL((k_step<0, 9>), dim3(heavy), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev, done_dev,
-                               info_dev, 0);
-        else if (e->lds_log == 11)
-            hipLaunchKernelGGL((k_step<0, 11>), dim3(heavy), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
-                               done_dev, info_dev, 0);
-        else
-            hipLaunchKernelGGL((k_step<0, 10>), dim3(heavy), dim3(64), 0, s, a, actions_dev, obs_dev, reward_dev,
-                               done_dev, info_dev, 0);
-        if (heavy < A.B) {
-            CK(hipEventRecord(e->ev_join, e->side));
-            CK(hipStreamWaitEvent(s, e->ev_join, 0));
-        }
-        if (A.cls) {
-            hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, A.cls, e->perm, A.B);
-            e->perm_valid = true;
-        }
+        launch_step(e, s, a, A.B, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+        if (A.cls) launch_order(e, s);
     }
     CKL();
     return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
