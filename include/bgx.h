@@ -133,7 +133,8 @@ int bgx_set_lanes(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_
 int bgx_engine_error(bgx_engine* e, int32_t* err_out);
 
 /* ---- policy network (agent/policy_network.py:44-75) + select_action (ppo_agent.py:138-191) ----
- * Weights are packed once per update into MFMA operand order (fp32):
+ * Weights are packed once per update into MFMA operand order (f16 hi/lo split
+ * pairs with power-of-two scales; fp32-equivalent results, see bg_mlp.hip):
  * bgx_policy_packed_size(H, A) floats; H <= 128.  Inputs are torch nn.Linear
  * layouts: W1 [H][198], b1 [H], Wa [A][H], ba [A], wv [H], bv [1]. */
 int bgx_policy_packed_size(int32_t hidden, int32_t n_actions);
@@ -143,7 +144,7 @@ int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const flo
 /* One fused pass per game lane: features from the 64-byte lane record
  * (bgx_buffers.lanes layout), relu(W1 x + b1), logits = Wa h + ba, value = wv h + bv,
  * masked = logits + log(mask + 1e-45) with mask = [a < legal count], then
- * action ~ Categorical(softmax(masked)) (Gumbel-max on Philox(seed, step, row, a))
+ * action ~ Categorical(softmax(masked)) (Gumbel-max, noise hashed from (seed, step, row, a))
  * or argmax if greedy (eval mode, ppo_agent.py:188-191).  act_out int32[n],
  * logp_out float[n] (log softmax(masked)[action]), value_out float[n];
  * logits_out float[n][32*ceil((A+1)/32)] (raw logits, value at column A) may be

@@ -21,6 +21,18 @@
 
 namespace bg {
 
+// Work counters for experiments (built with -DBGX_COUNTERS only).
+#ifdef BGX_COUNTERS
+__device__ unsigned long long g_cnt[16];
+#define BG_CNT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&bg::g_cnt[i], (unsigned long long)(v)); } while (0)
+#define BG_T0(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define BG_T1(i, t) BG_CNT(i, __builtin_amdgcn_s_memtime() - t)
+#else
+#define BG_CNT(i, v) do { } while (0)
+#define BG_T0(t) do { } while (0)
+#define BG_T1(i, t) do { } while (0)
+#endif
+
 constexpr int kBar = 24;   // moves/move_types.py:33
 constexpr int kOff = 25;   // moves/move_types.py:34
 constexpr uint32_t kHome[2] = {0xFC0000u, 0x3Fu};   // P1 home 18..23, P2 home 0..5 (conditions.py:122-126)
@@ -131,6 +143,18 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t a, uint32_t b, uint32_t c,
     return h;
 }
 
+// Key tests as xor/or reductions ending in ONE compare.  The empty asm hides the
+// reduction from LLVM, which otherwise re-forms a <4 x i32> compare and expands
+// it into per-word compares, cndmasks and 16-bit mask arithmetic.
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+    __asm__("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ bool key_eq(const uint4& v, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return opaque((v.x ^ a) | (v.y ^ b) | (v.z ^ c) | (v.w ^ d)) == 0u;
+}
+__device__ __forceinline__ bool key_empty(const uint4& v) { return opaque(v.x | v.y | v.z | v.w) == 0u; }
+
 // Open addressing, linear probing, empty == all-zero key (a real afterstate
 // always has a non-zero own count/bar/off).  The whole wave probes 64
 // consecutive slots per step.  Never more than 7/8 full (callers enforce).
@@ -143,8 +167,8 @@ __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b
     for (;;) {
         const uint32_t slot = (base + (uint32_t)lane) & mask;
         const uint4 v = tab[slot];
-        const bool eq = v.x == a && v.y == b && v.z == c && v.w == d;
-        const bool em = (v.x | v.y | v.z | v.w) == 0u;
+        const bool eq = key_eq(v, a, b, c, d);
+        const bool em = key_empty(v);
         const uint64_t beq = __ballot(eq), bem = __ballot(em);
         if (beq) return false;                 // no deletions: a match precedes any empty
         if (bem) {
@@ -164,8 +188,8 @@ __device__ __forceinline__ bool table_contains_lane(SlotPtr tab, uint32_t a, uin
     uint32_t h = key_hash(a, b, c, d) & mask;
     for (;;) {
         const uint4 v = tab[h];
-        if (v.x == a && v.y == b && v.z == c && v.w == d) return true;
-        if ((v.x | v.y | v.z | v.w) == 0u) return false;
+        if (key_eq(v, a, b, c, d)) return true;
+        if (key_empty(v)) return false;
         h = (h + 1u) & mask;
     }
 }
@@ -175,43 +199,72 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, int lane) {
 }
 
 // Per-lane lookup that also reports where the key would go: on a miss, `slot`
-// is the first empty slot of the key's probe sequence.
+// is the first empty slot of the key's probe sequence.  Four consecutive slots
+// per step (independent LDS reads in flight): the chain walk of a loaded table
+// costs a quarter of the dependent round trips.
 template <int LOG_SLOTS, typename SlotPtr>
 __device__ __forceinline__ bool probe_lane(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
                                            uint32_t& slot) {
     constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
     uint32_t h = key_hash(a, b, c, d) & mask;
     for (;;) {
-        const uint4 v = tab[h];
-        if (v.x == a && v.y == b && v.z == c && v.w == d) { slot = h; return true; }
-        if ((v.x | v.y | v.z | v.w) == 0u) { slot = h; return false; }
-        h = (h + 1u) & mask;
+        uint4 v0 = tab[h], v1 = tab[(h + 1u) & mask], v2 = tab[(h + 2u) & mask], v3 = tab[(h + 3u) & mask];
+        // all four reads in flight before the first use (one wait, not four)
+        __asm__ volatile("" : "+v"(v0.x), "+v"(v1.x), "+v"(v2.x), "+v"(v3.x));
+        const uint32_t meq = (uint32_t)key_eq(v0, a, b, c, d) | ((uint32_t)key_eq(v1, a, b, c, d) << 1) |
+                             ((uint32_t)key_eq(v2, a, b, c, d) << 2) | ((uint32_t)key_eq(v3, a, b, c, d) << 3);
+        const uint32_t mem = (uint32_t)key_empty(v0) | ((uint32_t)key_empty(v1) << 1) |
+                             ((uint32_t)key_empty(v2) << 2) | ((uint32_t)key_empty(v3) << 3);
+        const uint32_t stop = meq | mem;
+        if (stop) {
+            const uint32_t q = (uint32_t)__builtin_ctz(stop);
+            slot = (h + q) & mask;
+            return (meq >> q) & 1u;
+        }
+        h = (h + 4u) & mask;
     }
 }
 
-// Insert the keys of the lanes in `fresh` -- pairwise distinct and all absent,
-// each lane's `slot` from probe_lane against the current table -- in lane
-// order.  A lane whose empty slot was just taken moves on to the next empty
-// slot of its own probe sequence (linear probing stays valid).
-template <int LOG_SLOTS, typename SlotPtr>
-__device__ __forceinline__ void place_absent(SlotPtr tab, uint64_t fresh, uint32_t a, uint32_t b, uint32_t c,
-                                             uint32_t d, uint32_t slot) {
+// Insert the keys of the lanes in `fresh`, each lane's `slot` from probe_lane
+// against the current table (all absent).  Rounds: among the pending lanes the
+// lowest lane targeting a slot wins it and all winners write at once; a loser
+// finds its slot taken -- with DEDUP (keys may repeat: cousins from different
+// parents) it drops out if the winner's key equals its own, otherwise it
+// re-probes (checking equality too) to the next empty slot of its own probe
+// sequence, and competes in the next round.  Returns `fresh` minus duplicates;
+// the kept lane of equal keys is the lowest (equal keys share their probe
+// chain, so they always meet on the same slot).  Linear probing stays valid.
+template <int LOG_SLOTS, bool DEDUP, typename SlotPtr>
+__device__ __forceinline__ uint64_t place_batch(SlotPtr tab, uint64_t fresh, uint32_t a, uint32_t b, uint32_t c,
+                                                uint32_t d, uint32_t slot) {
     constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
     const int lane = threadIdx.x & 63;
-    while (fresh) {
-        const int src = __ffsll((unsigned long long)fresh) - 1;
-        fresh &= fresh - 1;
-        const uint32_t hs = rdl(slot, src);
-        if (lane == src) tab[hs] = make_uint4(a, b, c, d);
+    uint64_t pend = fresh;
+    while (pend) {
+        bool win = (pend >> lane) & 1ull;
+        for (uint64_t m = pend; m; m &= m - 1ull) {
+            const int src = __ffsll((unsigned long long)m) - 1;
+            const uint32_t hs = rdl(slot, src);
+            win = win && !(src < lane && slot == hs);
+        }
+        if (win) tab[slot] = make_uint4(a, b, c, d);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (((fresh >> lane) & 1ull) && slot == hs) {
+        pend &= ~__ballot(win);
+        if (!pend) break;
+        bool drop = false;
+        if ((pend >> lane) & 1ull) {
             for (;;) {
-                slot = (slot + 1u) & mask;
                 const uint4 v = tab[slot];
-                if ((v.x | v.y | v.z | v.w) == 0u) break;
+                if (DEDUP && key_eq(v, a, b, c, d)) { drop = true; break; }
+                if (key_empty(v)) break;
+                slot = (slot + 1u) & mask;
             }
         }
+        const uint64_t dups = __ballot(drop);
+        pend &= ~dups;
+        fresh &= ~dups;
     }
+    return fresh;
 }
 
 __device__ __forceinline__ int lane_rank(uint64_t m) {          // set bits of m below this lane
@@ -244,12 +297,12 @@ __device__ __forceinline__ Node rd_node(const Node& t, int src) {
 // got4 is off, and got4 off now means it was off throughout the first visit;
 // 4-long leaves are attempted unconditionally), so all of them are duplicates
 // and the revisit is a no-op: skip it.  Memo tables are per depth (2 and 3),
-// 256 slots each in LDS; when one fills up it stops recording (still exact).
-#ifndef BGX_LOG_MEMO
-#define BGX_LOG_MEMO 8
-#endif
-constexpr int kLogMemo = BGX_LOG_MEMO;
-constexpr int kMemoCap = (7 << kLogMemo) / 8;
+// in LDS, 128 slots at depth 2 and 512 at depth 3 (a big doubles position has
+// ~60-130 distinct depth-2 states and ~250-700 at depth 3; a nearly full table
+// means long probe chains); when one fills up it stops recording (still exact).
+constexpr int kLogMemo2 = 7, kLogMemo3 = 9;
+constexpr int kMemoSlots = (1 << kLogMemo2) + (1 << kLogMemo3);    // memo2 = [0, 128), memo3 = [128, 640)
+constexpr int kMemoCap2 = (7 << kLogMemo2) / 8, kMemoCap3 = (7 << kLogMemo3) / 8;
 
 // Where surviving entries go.  MoveSink: the env's ordered move list in HBM
 // (first `cap` entries).  Other sinks (bg_search.hip) keep afterstate keys.
@@ -314,17 +367,23 @@ struct Gen {
     }
 
     // Add the entries of the lanes in `fresh` (length len), in lane order.
+    // DEDUP: the batch may hold equal keys (cousins); first one wins.
+    template <bool DEDUP = false>
     __device__ __forceinline__ void commit(uint64_t fresh, const Node& t, uint64_t enc, uint32_t slot, int len) {
-        const int n = __popcll(fresh);
+        int n = __popcll(fresh);
         if (!n) return;
+        BG_T0(tc);
         if (fill() + n >= cap_unique) { ovf = true; return; }
-        place_absent<LOG_SLOTS>(tab, fresh, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        fresh = place_batch<LOG_SLOTS, DEDUP>(tab, fresh, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        if (DEDUP) n = __popcll(fresh);
+        BG_CNT(8, n);
         n_unique += n;
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
             sink.push_lanes(fresh, t, enc, count);
             count += n;
         }
+        BG_T1(13, tc);
     }
 
     // Siblings (children of one node) are pairwise distinct afterstates
@@ -339,13 +398,46 @@ struct Gen {
         commit(__ballot(act && !found), t, enc, slot, len);
     }
 
+    // Leaves of two nodes in one batch: lanes 0..31 = child bit l of node A,
+    // lanes 32..63 = child bit l-32 of node B (bit 31 = the special move), so
+    // lane order is child order, A before B.  Cousins may coincide: DEDUP commit.
+    __device__ __forceinline__ void pair_batch(const Node& sA, const Kids& kA, uint64_t pA, const Node& sB,
+                                               const Kids& kB, uint64_t pB, int d, int shift, int len) {
+        const int l = threadIdx.x & 63;
+        const bool hb = l >= 32;
+        const int bit = l & 31;
+        const uint32_t bits = hb ? kB.bits : kA.bits;
+        const bool act = (bits >> bit) & 1u;
+        Node t;
+        uint64_t enc = 0;
+        if (act) {
+            const Node& s = hb ? sB : sA;
+            const Kids k{bits, hb ? kB.extra : kA.extra};
+            const Sub m = child(s, k, bit, d, pl);
+            t = apply(s, m, pl);
+            enc = (hb ? pB : pA) | ((uint64_t)m.enc << shift);
+        }
+        BG_CNT(6, 1);
+        BG_CNT(7, __popc(kA.bits) + __popc(kB.bits));
+        BG_T0(tp);
+        uint32_t slot = 0;
+        bool found = true;
+        if (act) found = probe_lane<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        commit<true>(__ballot(act && !found), t, enc, slot, len);
+        BG_T1(14, tp);
+    }
+
     // All children of s as entries prefix | enc << shift of length len.
     __device__ __forceinline__ void leaf_batch(const Node& s, const Kids& k, int d, uint64_t prefix, int shift,
                                                int len) {
         Node t;
         uint32_t e = 0;
         const bool act = lane_child(s, k, d, t, e);
+        BG_CNT(6, 1);
+        BG_CNT(7, __popc(k.bits));
+        BG_T0(tp);
         batch(act, t, prefix | ((uint64_t)e << shift), len);
+        BG_T1(14, tp);
     }
 
     // handle_non_doubles (handle_moves.py:109-200); the pre-scan (:144-155) is
@@ -373,24 +465,26 @@ struct Gen {
 
     // Revisit check of a sibling batch at one depth: returns the lanes not seen
     // before and records them (while the memo has room).
+    template <int LOGM>
     __device__ __forceinline__ uint64_t memo_batch(uint4* memo, int& nm, bool act, const Node& t, uint32_t tag) {
         if (!memo) return __ballot(act);
+        constexpr int cap = (7 << LOGM) / 8;
         uint32_t slot = 0;
         bool found = true;
         const uint32_t k3 = TAGGED ? t.k3 ^ tag : t.k3;
         if (act) {
             if (TAGGED) found = probe_lane<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
-            else found = probe_lane<kLogMemo>(memo, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            else found = probe_lane<LOGM>(memo, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
         }
         const uint64_t fresh = __ballot(act && !found);
         uint64_t rec = fresh;
         int n = __popcll(rec);
-        int room = kMemoCap - nm;
+        int room = cap - nm;
         if (TAGGED) room = min(room, cap_unique / 3 - n_memo2 - n_memo3);
         while (n > room && rec) { rec &= ~(1ull << (63 - __clzll((long long)rec))); --n; }
         if (rec) {
-            if (TAGGED) place_absent<LOG_SLOTS>(tab, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
-            else place_absent<kLogMemo>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            if (TAGGED) place_batch<LOG_SLOTS, false>(tab, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            else place_batch<LOGM, false>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
         }
         nm += n;
         return fresh;
@@ -401,7 +495,13 @@ struct Gen {
     // Each node's children are expanded one per lane (state, revisit check,
     // next-level child list); the walk itself stays in order.
     __device__ __forceinline__ void doubles(const Node& s0, int d) {
+        BG_T0(td);
+        doubles_(s0, d);
+        BG_T1(1, td);
+    }
+    __device__ __forceinline__ void doubles_(const Node& s0, int d) {
         bool got4 = false;
+        BG_CNT(0, 1);
         const Kids k1 = gen(s0, d, pl, blocked);
         Node t1;
         uint32_t e1 = 0;
@@ -421,7 +521,8 @@ struct Gen {
             Node t2;
             uint32_t e2l = 0;
             const bool a2 = lane_child(s1, k2, d, t2, e2l);
-            const uint64_t f2 = memo_batch(memo2, n_memo2, a2, t2, kTag2);
+            const uint64_t f2 = memo_batch<kLogMemo2>(memo2, n_memo2, a2, t2, kTag2);
+            BG_CNT(2, 1); BG_CNT(3, __popcll(f2)); BG_CNT(11, __popc(k2.bits));
             uint32_t q3 = 0;
             int x3 = -1;
             if ((f2 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; x3 = k.extra; }
@@ -434,13 +535,16 @@ struct Gen {
                     if (!got4) { insert(s2, m2, 2); if (ovf) return; }
                     continue;
                 }
+                BG_T0(tx);
                 Node t3;
                 uint32_t e3l = 0;
                 const bool a3 = lane_child(s2, k3, d, t3, e3l);
-                const uint64_t f3 = memo_batch(memo3, n_memo3, a3, t3, kTag3);
+                const uint64_t f3 = memo_batch<kLogMemo3>(memo3, n_memo3, a3, t3, kTag3);
+                BG_CNT(4, 1); BG_CNT(5, __popcll(f3)); BG_CNT(12, __popc(k3.bits));
                 uint32_t q4 = 0;
                 int x4 = -1;
                 if ((f3 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; x4 = k.extra; }
+                BG_T1(15, tx);
                 for (uint64_t b3 = f3; b3; b3 &= b3 - 1ull) {
                     const int i3 = __ffsll((unsigned long long)b3) - 1;
                     const Kids k4{rdl(q4, i3), (int)rdl((uint32_t)x4, i3)};
@@ -449,7 +553,19 @@ struct Gen {
                         if (!got4) { insert(rd_node(t3, i3), m3, 3); if (ovf) return; }
                         continue;
                     }
-                    leaf_batch(rd_node(t3, i3), k4, d, m3, 48, 4);
+                    // got4 holds from this node's leaves on, so dead ends up to the
+                    // next node with children are no-ops: pair the two nodes' leaves
+                    const uint64_t withkids = __ballot(((f3 >> (threadIdx.x & 63)) & 1ull) && q4 != 0u);
+                    const uint64_t later = withkids & (b3 & (b3 - 1ull));
+                    if (later) {
+                        const int j3 = __ffsll((unsigned long long)later) - 1;
+                        const Kids kB{rdl(q4, j3), (int)rdl((uint32_t)x4, j3)};
+                        const uint64_t mB = m2 | ((uint64_t)rdl(e3l, j3) << 32);
+                        pair_batch(rd_node(t3, i3), k4, m3, rd_node(t3, j3), kB, mB, d, 48, 4);
+                        b3 &= ~((2ull << j3) - 1ull) | (1ull << i3);   // drop everything up to j3 (i3 by the loop)
+                    } else {
+                        leaf_batch(rd_node(t3, i3), k4, d, m3, 48, 4);
+                    }
                     if (ovf) return;
                     got4 = true;
                 }

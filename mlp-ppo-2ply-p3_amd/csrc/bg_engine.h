@@ -199,12 +199,12 @@ __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint6
     for (int i = lane_id(); i < slots; i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = r0 == r1;
     if (memo && dbl && !TAGGED)
-        for (int i = lane_id(); i < (2 << kLogMemo); i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = lane_id(); i < kMemoSlots; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     Gen<LOG, SlotPtr, MoveSink, TAGGED> g;
     g.tab = tab; g.sink.out = out; g.sink.cap = cap; g.pl = pl; g.cap_unique = cap_unique;
     g.memo2 = memo && dbl ? memo : nullptr;
-    g.memo3 = memo && dbl ? (TAGGED ? memo : memo + (1 << kLogMemo)) : nullptr;
+    g.memo3 = memo && dbl ? (TAGGED ? memo : memo + (1 << kLogMemo2)) : nullptr;
     uint32_t blocked;
     const Node s0 = node_from_bytes(bv, pl, blocked);
     g.blocked = blocked;

@@ -34,7 +34,7 @@ template <int PHASE, int LOG, int MEMO = 1>
 __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
                                              int32_t* info, int base) {
     __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo_[MEMO == 1 ? (2 << kLogMemo) : 1];
+    __shared__ uint4 memo_[MEMO == 1 ? kMemoSlots : 1];
     uint4* memo = MEMO == 1 ? memo_ : MEMO == 2 ? tab : nullptr;
     const int bi = (int)blockIdx.x + base;
     const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : bi;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
 template <int LOG>
 __global__ __launch_bounds__(64) void k_reset(Args A, const uint8_t* lane_mask, float* obs, int mark_only) {
     __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo[2 << kLogMemo];
+    __shared__ uint4 memo[kMemoSlots];
     const int gi = blockIdx.x;
     int bv = load_rec(A, gi);
     uint64_t ctr = A.dice_mode == BGX_DICE_PHILOX ? A.ctr[gi] : 0;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(64) void k_movegen(const int8_t* boards, const uint
                                                 int n, int cap, int16_t* nmoves, int32_t* ntotal, uint64_t* moves,
                                                 int32_t* ovf_count, int32_t* ovf_queue) {
     __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo[2 << kLogMemo];
+    __shared__ uint4 memo[kMemoSlots];
     const int gi = blockIdx.x;
     const int l = lane_id();
     const int bv = l < 52 ? (int)boards[(size_t)gi * 52 + l] : 0;
@@ -208,7 +208,7 @@ template <int SRC, int TIER>
 __global__ __launch_bounds__(64) void k_movegen_over(Args A, const int8_t* boards, const uint8_t* players,
                                                      const uint8_t* dice, int cap, int16_t* nmoves, int32_t* ntotal,
                                                      uint64_t* moves, uint4* tables) {
-    __shared__ uint4 memo[2 << kLogMemo];
+    __shared__ uint4 memo[kMemoSlots];
     __shared__ uint4 lds_tab[TIER == 1 ? (1 << kLogMid) : 1];
     uint4* tab = TIER == 1 ? lds_tab : tables + ((size_t)blockIdx.x << kLogSlotsSlow);
     const int count = (int)ufl((uint32_t)A.ovf_count[TIER - 1]);
@@ -322,7 +322,7 @@ __global__ void k_action_masks(Args A, int16_t* counts, float* masks) {
 template <int LOG>
 __global__ __launch_bounds__(64) void k_regen(Args A, int lane0) {
     __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo[2 << kLogMemo];
+    __shared__ uint4 memo[kMemoSlots];
     const int gi = lane0 + blockIdx.x;
     int bv = load_rec(A, gi);
     const int cur = rd(bv, R_CUR), r0 = rd(bv, R_ROLL0), r1 = rd(bv, R_ROLL1);
@@ -518,6 +518,16 @@ int bgx_engine_mt_state(bgx_engine* e, int32_t lane, uint32_t* state_host, int32
     else CK(hipMemcpy(state_host, dev, 625 * 4, hipMemcpyDeviceToHost));
     return BGX_OK;
 }
+
+#ifdef BGX_COUNTERS
+extern "C" int bgx_debug_counters(unsigned long long* out16) {
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bg::g_cnt), 16 * 8));
+    unsigned long long z[16] = {0};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z, 16 * 8));
+    return BGX_OK;
+}
+#endif
 
 // diagnostics: copy the per-lane [start, end] s_memrealtime stamps of the last step
 extern "C" int bgx_debug_stamps(bgx_engine* e, uint64_t* host_out) {

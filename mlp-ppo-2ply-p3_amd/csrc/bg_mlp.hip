@@ -2,17 +2,23 @@
 // fused with the feature encoder and select_action's masked sampling
 // (agent/ppo_agent.py:164-187).
 //
-// One wave = 32 game rows.  GEMM1 computes X1 = W1 . F^T (hidden x rows) with
-// v_mfma_f32_32x32x2_f32, the B operand (features) generated on the fly from the
-// rows' int8 lane records staged in LDS.  The accumulator layout of X1 (column =
-// row on the lane, hidden units in registers) is used UNMOVED as the B operand of
-// GEMM2 (Y = W2 . X1, W2 = [action_head; value_head]): the host packs W2's
-// columns in the k order the accumulator registers deliver.  Each lane then
-// owns 16 outputs of one row per 32-row output tile, so masked log-sum-exp and
-// Gumbel-max sampling run in registers with one cross-half shuffle per row.
+// One wave = 32 game rows.  GEMM1 computes X1 = W1 . F^T (hidden x rows), the B
+// operand (features) generated on the fly from the rows' int8 lane records
+// staged in LDS.  The accumulator layout of X1 (column = row on the lane, hidden
+// units in registers) is used UNMOVED as the B operand of GEMM2
+// (Y = W2 . X1, W2 = [action_head; value_head]): the host packs W2's columns in
+// the k order the accumulator registers deliver.  Each lane then owns 16
+// outputs of one row per 32-row output tile, so the masked log-sum-exp and the
+// Gumbel-max draw run in registers with one cross-half shuffle per row.
 //
-// f32-input MFMA is an exact f32 FMA chain (cdna_hip_programming.md §3), so the
-// logits/values match torch fp32 to ~1e-6 (tests/test_gpu_policy.py).
+// Precision: fp32 semantics from f16 MFMA (v_mfma_f32_32x32x16_f16, 16x the
+// f32-MFMA rate).  Every operand x is split x = hi + lo (hi = f16(x),
+// lo = f16(x - hi)) and a product is hi*hi + hi*lo + lo*hi: 22 significant bits
+// per operand, products exact in the f32 accumulator, the dropped lo*lo term
+// below 2^-22 relative.  Power-of-two scales keep the parts in f16's normal
+// range: per weight matrix (pack time, max |w| -> [2^13, 2^14)) and per wave for
+// the hidden layer; they are undone exactly.  Logits/values match torch fp32 to
+// ~1e-6 (tests/test_gpu_policy.py asserts 1e-5).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../include/bgx.h"
@@ -20,10 +26,12 @@
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kIn = 198;
-constexpr int kK1 = kIn / 2;          // 99 k-steps of 32x32x2
+constexpr int kKB1 = (kIn + 15) / 16;     // 13 k-blocks of 16 (features padded to 208)
 constexpr float kMaskLog = -103.27892990343185f;  // log(fp32(1e-45)) (ppo_agent.py:166)
+constexpr int kHdr = 16;                  // header floats: [0] = e1, [1] = e2 (int bits)
 
 __constant__ float kOff15m[16] = {
     0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
@@ -32,8 +40,9 @@ __constant__ float kOff15m[16] = {
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// feature k (0..197) of the row whose 64-byte record starts at rec (LDS)
+// feature k (0..197; 0 beyond) of the row whose 64-byte record starts at rec (LDS)
 __device__ __forceinline__ float feat(const uint8_t* rec, int k) {
+    if (k >= kIn) return 0.0f;
     if (k >= 196) return (k == 196) == (rec[52] == 0) ? 1.0f : 0.0f;
     const int p = k >= 98 ? 1 : 0;
     const int g = k - 98 * p;
@@ -47,41 +56,88 @@ __device__ __forceinline__ float feat(const uint8_t* rec, int k) {
     return kOff15m[rec[50 + p] & 15];
 }
 
-__device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) { return __umulhi(a, b); }
-
-// Philox4x32-10 -> 4 uniforms strictly inside (0,1)
-__device__ __forceinline__ void philox4(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
-                                        uint32_t k1, float u[4]) {
-    #pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t h0 = mulhi(0xD2511F53u, c0), l0 = 0xD2511F53u * c0;
-        const uint32_t h1 = mulhi(0xCD9E8D57u, c2), l1 = 0xCD9E8D57u * c2;
-        c0 = h1 ^ c1 ^ k0; c1 = l1; c2 = h0 ^ c3 ^ k1; c3 = l0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-    const uint32_t w[4] = {c0, c1, c2, c3};
-    #pragma unroll
-    // 23 bits + 1/2: exactly representable, u in [2^-24, 1 - 2^-24] (never 0 or 1)
-    for (int i = 0; i < 4; ++i) u[i] = ((float)(w[i] >> 9) + 0.5f) * (1.0f / 8388608.0f);
+__device__ __forceinline__ void split(float x, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)x;
+    lo = (_Float16)(x - (float)hi);
 }
 
-// Packed weights (bgx_policy_pack):
-//   w1p [99][T][64]       w1p[kk][t][l] = W1[32t + (l&31)][2kk + (l>>5)]
-//   b1p [T][16][64]       b1p[t][r][l]  = b1[32t + hid(r, l>>5)]
-//   w2p [OT][16T][64]     w2p[o][kk][l] = W2[32o + (l&31)][32(kk/16) + hid(kk%16, l>>5)]
-//   b2p [OT][16][64]      b2p[o][r][l]  = b2[32o + hid(r, l>>5)]
-// with hid(r, h) = (r&3) + 8(r>>2) + 4h (the 32x32 accumulator row map) and
-// W2 = [action_head.weight; value_head.weight; 0], b2 likewise (OT*32 rows).
+__device__ __forceinline__ f16x8 as_h8(uint4 v) { return __builtin_bit_cast(f16x8, v); }
+
+// exponent e with max_abs * 2^e in [2^13, 2^14) (0 for 0 / non-finite)
+__device__ __forceinline__ int scale_exp(float max_abs) {
+    if (!(max_abs > 0.0f) || !(max_abs < INFINITY)) return 0;
+    int q;
+    (void)frexpf(max_abs, &q);
+    const int e = 14 - q;
+    return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
+
+// 32-bit mixer (lowbias32): a bijection with good avalanche; noise for the
+// Gumbel-max draw keyed by (seed, step, row, action)
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+    return x;
+}
+
+// v_log_f32 / v_exp_f32 directly (base 2): every argument below is a normal float
+__device__ __forceinline__ float fast_ln(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+// Gumbel(0,1) = -log(E), E = -log(u) ~ Exp(1), u = ((w >> 9) + 1/2) 2^-23 in (0,1).
+// For u close to 1, -log(u) = v + v^2/2 + v^3/3 with v = 1 - u (exact), so E keeps
+// full relative precision where the hardware log would lose it.
+__device__ __forceinline__ float gumbel(uint32_t w) {
+    const float u = ((float)(w >> 9) + 0.5f) * (1.0f / 8388608.0f);
+    const float v = 1.0f - u;
+    const float series = v * (1.0f + v * (0.5f + v * (1.0f / 3.0f)));
+    const float e = v < (1.0f / 64.0f) ? series : -fast_ln(u);
+    return -fast_ln(e);
+}
+
+// Packed layout (bgx_policy_pack), in floats:
+//   hdr  [16]                       e1, e2 (int bits)
+//   w1q  [13][T][2][64] x uint4     lane l: W1s[32t + (l&31)][16kb + 8(l>>5) + i], i = 0..7, part 0 = hi, 1 = lo
+//   b1p  [T][16][64] f32            b1[32t + hid(r, l>>5)] * 2^e1
+//   w2q  [OT][T][2][2][64] x uint4  lane l, sub-block m: W2s[32o + (l&31)][32t + hid(8m + i, l>>5)]
+//   b2p  [OT][16][64] f32           b2[32o + hid(r, l>>5)]  (unscaled)
+// with W1s = W1 * 2^e1, W2s = W2 * 2^e2, hid(r, h) = (r&3) + 8(r>>2) + 4h (the
+// 32x32 accumulator row map), W2 = [action_head.weight; value_head.weight; 0].
 __device__ __forceinline__ int hid(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+struct PackView {
+    const int* hdr;
+    const uint4* w1q;
+    const float* b1p;
+    const uint4* w2q;
+    const float* b2p;
+};
+
+__host__ __device__ inline int sz_w1q(int T) { return kKB1 * T * 2 * 64 * 4; }
+__host__ __device__ inline int sz_b1p(int T) { return T * 16 * 64; }
+__host__ __device__ inline int sz_w2q(int T, int OT) { return OT * T * 2 * 2 * 64 * 4; }
+__host__ __device__ inline int sz_b2p(int OT) { return OT * 16 * 64; }
+
+template <typename P>
+__host__ __device__ inline void views(P base, int T, int OT, P& hdr, P& w1q, P& b1p, P& w2q, P& b2p) {
+    hdr = base;
+    w1q = hdr + kHdr;
+    b1p = w1q + sz_w1q(T);
+    w2q = b1p + sz_b1p(T);
+    b2p = w2q + sz_w2q(T, OT);
+}
+
 template <int T>
-__global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ recs, int n, const float* __restrict__ w1p,
-                                                   const float* __restrict__ b1p, const float* __restrict__ w2p,
-                                                   const float* __restrict__ b2p, int n_actions, int n_otiles,
+__global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ recs, int n,
+                                                   const float* __restrict__ packed, int n_actions, int n_otiles,
                                                    uint32_t seed_lo, uint32_t seed_hi, uint32_t step, int greedy,
                                                    int32_t* act_out, float* logp_out, float* value_out,
                                                    float* logits_out) {
     __shared__ uint8_t srec[32 * 64];
+    const float *hdrf, *w1f, *b1p, *w2f, *b2p;
+    views(packed, T, n_otiles, hdrf, w1f, b1p, w2f, b2p);
+    const uint4* w1q = (const uint4*)w1f;
+    const uint4* w2q = (const uint4*)w2f;
+    const int e1 = __builtin_bit_cast(int, hdrf[0]), e2 = __builtin_bit_cast(int, hdrf[1]);
     const int l = lane_id();
     const int row0 = blockIdx.x * 32;
     // stage 32 records (2 KiB): lane l copies 32 bytes
@@ -98,65 +154,110 @@ __global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ r
     const uint8_t* myrec = srec + j * 64;
     const int count = (int)myrec[60] | ((int)myrec[61] << 8);
 
-    // ---- GEMM1: X1[t] = W1[32t..32t+31, :] . F^T  (+ b1, ReLU)
+    // ---- GEMM1: X1s[t] = W1s[32t.., :] . F^T + b1 * 2^e1  (= 2^e1 X1)
     f32x16 x1[T];
     #pragma unroll
     for (int t = 0; t < T; ++t)
         #pragma unroll
         for (int r = 0; r < 16; ++r) x1[t][r] = b1p[(t * 16 + r) * 64 + l];
-    for (int kk = 0; kk < kK1; ++kk) {
-        const float b = feat(myrec, 2 * kk + h);
+    for (int kb = 0; kb < kKB1; ++kb) {
+        f16x8 bh, bl;
+        #pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            _Float16 a, b;
+            split(feat(myrec, 16 * kb + 8 * h + i), a, b);
+            bh[i] = a; bl[i] = b;
+        }
         #pragma unroll
         for (int t = 0; t < T; ++t) {
-            const float a = w1p[(kk * T + t) * 64 + l];
-            x1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, x1[t], 0, 0, 0);
+            const f16x8 ah = as_h8(w1q[((kb * T + t) * 2 + 0) * 64 + l]);
+            const f16x8 al = as_h8(w1q[((kb * T + t) * 2 + 1) * 64 + l]);
+            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, x1[t], 0, 0, 0);
+            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, x1[t], 0, 0, 0);
+            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, x1[t], 0, 0, 0);
         }
     }
+    // ReLU, then a per-wave scale 2^ex for the split of the hidden layer
+    float mx = 0.0f;
     #pragma unroll
     for (int t = 0; t < T; ++t)
         #pragma unroll
-        for (int r = 0; r < 16; ++r) x1[t][r] = fmaxf(x1[t][r], 0.0f);
+        for (int r = 0; r < 16; ++r) { x1[t][r] = fmaxf(x1[t][r], 0.0f); mx = fmaxf(mx, x1[t][r]); }
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) mx = fmaxf(mx, __shfl_xor(mx, d));
+    const int ex = scale_exp(mx);
+    f16x8 xh[T][2], xl[T][2];
+    #pragma unroll
+    for (int t = 0; t < T; ++t)
+        #pragma unroll
+        for (int m = 0; m < 2; ++m)
+            #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                _Float16 a, b;
+                split(ldexpf(x1[t][8 * m + i], ex), a, b);
+                xh[t][m][i] = a; xl[t][m][i] = b;
+            }
+    // Y' = W2s . (2^(e1+ex) X1) + b2 2^E = 2^E Y,  E = e2 + e1 + ex
+    const int E = e2 + e1 + ex;
+    const float up = ldexpf(1.0f, E), down = ldexpf(1.0f, -E);
 
     // ---- GEMM2 per 32-output tile + online masked log-sum-exp + Gumbel-max
+    // (branch-free: outputs that are not actions of this lane enter as -inf)
     float m = -INFINITY, s = 0.0f, best = -INFINITY, bestz = 0.0f, value = 0.0f;
     int besta = 0;
     const int grow = row0 + j;
+    const uint32_t rowkey = mix32(mix32(seed_lo ^ mix32(seed_hi + 0x9E3779B9u)) ^ step) ^ (uint32_t)grow * 0x85EBCA6Bu;
+    constexpr int NF = T * 2 * 2;                      // weight fragments per output tile
+    uint4 wcur[NF], wnxt[NF];
+    #pragma unroll
+    for (int f = 0; f < NF; ++f) wcur[f] = w2q[(size_t)f * 64 + l];
     for (int o = 0; o < n_otiles; ++o) {
+        // prefetch the next tile's fragments behind this tile's MFMAs
+        const int on = o + 1 < n_otiles ? o + 1 : o;
+        #pragma unroll
+        for (int f = 0; f < NF; ++f) wnxt[f] = w2q[((size_t)on * NF + f) * 64 + l];
         f32x16 y;
         #pragma unroll
-        for (int r = 0; r < 16; ++r) y[r] = b2p[(o * 16 + r) * 64 + l];
-        const float* wo = w2p + (size_t)o * (16 * T) * 64 + l;
+        for (int r = 0; r < 16; ++r) y[r] = b2p[(o * 16 + r) * 64 + l] * up;
         #pragma unroll
-        for (int t = 0; t < T; ++t) {
+        for (int t = 0; t < T; ++t)
             #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float a = wo[(t * 16 + r) * 64];
-                y = __builtin_amdgcn_mfma_f32_32x32x2f32(a, x1[t][r], y, 0, 0, 0);
+            for (int mm = 0; mm < 2; ++mm) {
+                const f16x8 ah = as_h8(wcur[(t * 2 + mm) * 2 + 0]);
+                const f16x8 al = as_h8(wcur[(t * 2 + mm) * 2 + 1]);
+                y = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh[t][mm], y, 0, 0, 0);
+                y = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl[t][mm], y, 0, 0, 0);
+                y = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[t][mm], y, 0, 0, 0);
             }
-        }
+        #pragma unroll
+        for (int f = 0; f < NF; ++f) wcur[f] = wnxt[f];
         // lane l holds outputs a = 32o + hid(r, h), r = 0..15, of row j
-        float u[16];
-        if (!greedy) {
-            #pragma unroll
-            for (int g = 0; g < 4; ++g)
-                philox4((uint32_t)grow, step, (uint32_t)(o * 8 + g * 2 + h), 0x504F4C59u, seed_lo, seed_hi, u + 4 * g);
-        }
+        float z[16];
+        float tm = -INFINITY;
         #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int a = 32 * o + hid(r, h);
-            const float z0 = y[r];
+            const float z0 = y[r] * down;
             if (logits_out && grow < n && a <= n_actions) logits_out[(size_t)grow * (32 * n_otiles) + a] = z0;
-            if (a == n_actions) value = z0;
-            if (a < n_actions) {
-                const float z = a < count ? z0 : z0 + kMaskLog;
-                const float mn = fmaxf(m, z);
-                s = s * __expf(m - mn) + __expf(z - mn);
-                m = mn;
-                // Gumbel(0,1) noise; accurate logf near u = 1
-                const float key = greedy ? z : z - logf(-logf(u[r]));
-                if (key > best) { best = key; besta = a; bestz = z; }
-            }
+            value = a == n_actions ? z0 : value;
+            z[r] = a < n_actions ? (a < count ? z0 : z0 + kMaskLog) : -INFINITY;
+            tm = fmaxf(tm, z[r]);
         }
+        const float mn = fmaxf(m, tm);
+        if (mn == -INFINITY) continue;                 // nothing of this lane's row so far
+        float acc = 0.0f;
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int a = 32 * o + hid(r, h);
+            acc += fast_exp(z[r] - mn);
+            const float key = greedy ? z[r] : z[r] + gumbel(mix32(rowkey ^ ((uint32_t)a * 0xC2B2AE35u)));
+            const bool up_ = key > best;
+            best = up_ ? key : best;
+            besta = up_ ? a : besta;
+            bestz = up_ ? z[r] : bestz;
+        }
+        s = s * fast_exp(m - mn) + acc;
+        m = mn;
     }
     // combine the two lane halves of each row (lanes j and j+32)
     const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(s, 32);
@@ -164,24 +265,50 @@ __global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ r
     const int besta2 = __shfl_xor(besta, 32);
     const float value2 = __shfl_xor(value, 32);
     const float mm = fmaxf(m, m2);
-    const float ss = s * __expf(m - mm) + s2 * __expf(m2 - mm);
+    const float ss = s * fast_exp(m - mm) + s2 * fast_exp(m2 - mm);
     const bool take2 = best2 > best || (best2 == best && besta2 < besta);
     const int a_fin = take2 ? besta2 : besta;
     const float z_fin = take2 ? bestz2 : bestz;
     const float v_fin = h == 0 ? value + value2 : 0.0f;   // the value row sits in exactly one half
     if (h == 0 && grow < n) {
         act_out[grow] = a_fin;
-        if (logp_out) logp_out[grow] = z_fin - (mm + __logf(ss));
+        if (logp_out) logp_out[grow] = z_fin - (mm + logf(ss));
         if (value_out) value_out[grow] = v_fin;
+    }
+}
+
+// max |w| of W1 and of W2 = [Wa; wv] -> header exponents (one workgroup)
+__global__ __launch_bounds__(1024) void k_policy_scale(const float* W1, const float* Wa, const float* wv, int H, int A,
+                                                       float* hdr) {
+    __shared__ float r1[16], r2[16];
+    const int t = threadIdx.x;
+    float m1 = 0.0f, m2 = 0.0f;
+    for (int i = t; i < H * kIn; i += 1024) m1 = fmaxf(m1, fabsf(W1[i]));
+    for (int i = t; i < A * H; i += 1024) m2 = fmaxf(m2, fabsf(Wa[i]));
+    for (int i = t; i < H; i += 1024) m2 = fmaxf(m2, fabsf(wv[i]));
+    #pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { m1 = fmaxf(m1, __shfl_xor(m1, d)); m2 = fmaxf(m2, __shfl_xor(m2, d)); }
+    if ((t & 63) == 0) { r1[t >> 6] = m1; r2[t >> 6] = m2; }
+    __syncthreads();
+    if (t == 0) {
+        for (int w = 1; w < 16; ++w) { m1 = fmaxf(m1, r1[w]); m2 = fmaxf(m2, r2[w]); }
+        hdr[0] = __builtin_bit_cast(float, scale_exp(m1));
+        hdr[1] = __builtin_bit_cast(float, scale_exp(m2));
+        for (int i = 2; i < kHdr; ++i) hdr[i] = 0.0f;
     }
 }
 
 // Pack torch-layout weights into the MFMA operand layouts above.
 __global__ void k_policy_pack(const float* W1, const float* b1, const float* Wa, const float* ba, const float* wv,
-                              const float* bv, int H, int A, int T, int OT, float* w1p, float* b1p, float* w2p,
-                              float* b2p) {
+                              const float* bv, int H, int A, int T, int OT, float* packed) {
+    float *hdr, *w1f, *b1p, *w2f, *b2p;
+    views(packed, T, OT, hdr, w1f, b1p, w2f, b2p);
+    const int e1 = __builtin_bit_cast(int, hdr[0]), e2 = __builtin_bit_cast(int, hdr[1]);
+    _Float16* w1h = (_Float16*)w1f;
+    _Float16* w2h = (_Float16*)w2f;
     const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int n1 = kK1 * T * 64, nb1 = T * 16 * 64, n2 = OT * 16 * T * 64, nb2 = OT * 16 * 64;
+    // one thread per (fragment, lane, element i) for the f16 parts; hi and lo written together
+    const int n1 = kKB1 * T * 64 * 8, nb1 = T * 16 * 64, n2 = OT * T * 2 * 64 * 8, nb2 = OT * 16 * 64;
     auto W2 = [&](int o, int k) -> float {
         if (k >= H) return 0.0f;
         if (o < A) return Wa[(size_t)o * H + k];
@@ -190,23 +317,31 @@ __global__ void k_policy_pack(const float* W1, const float* b1, const float* Wa,
     };
     auto B2 = [&](int o) -> float { return o < A ? ba[o] : (o == A ? bv[0] : 0.0f); };
     if (tid < n1) {
-        const int l = tid % 64, t = (tid / 64) % T, kk = tid / (64 * T);
-        const int hrow = 32 * t + (l & 31), k = 2 * kk + (l >> 5);
-        w1p[tid] = hrow < H ? W1[(size_t)hrow * kIn + k] : 0.0f;
+        const int i = tid % 8, l = (tid / 8) % 64, t = (tid / 512) % T, kb = tid / (512 * T);
+        const int hrow = 32 * t + (l & 31), k = 16 * kb + 8 * (l >> 5) + i;
+        const float w = hrow < H && k < kIn ? ldexpf(W1[(size_t)hrow * kIn + k], e1) : 0.0f;
+        _Float16 a, b;
+        split(w, a, b);
+        w1h[(((kb * T + t) * 2 + 0) * 64 + l) * 8 + i] = a;
+        w1h[(((kb * T + t) * 2 + 1) * 64 + l) * 8 + i] = b;
     } else if (tid < n1 + nb1) {
-        const int i = tid - n1;
-        const int l = i % 64, r = (i / 64) % 16, t = i / (64 * 16);
+        const int q = tid - n1;
+        const int l = q % 64, r = (q / 64) % 16, t = q / (64 * 16);
         const int hrow = 32 * t + hid(r, l >> 5);
-        b1p[i] = hrow < H ? b1[hrow] : 0.0f;
+        b1p[q] = hrow < H ? ldexpf(b1[hrow], e1) : 0.0f;
     } else if (tid < n1 + nb1 + n2) {
-        const int i = tid - n1 - nb1;
-        const int l = i % 64, kk = (i / 64) % (16 * T), o = i / (64 * 16 * T);
-        const int k = 32 * (kk / 16) + hid(kk % 16, l >> 5);
-        w2p[i] = W2(32 * o + (l & 31), k);
+        const int q = tid - n1 - nb1;
+        const int i = q % 8, l = (q / 8) % 64, mm = (q / 512) % 2, t = (q / 1024) % T, o = q / (1024 * T);
+        const int k = 32 * t + hid(8 * mm + i, l >> 5);
+        _Float16 a, b;
+        split(ldexpf(W2(32 * o + (l & 31), k), e2), a, b);
+        const size_t f = (((size_t)(o * T + t) * 2 + mm) * 2) * 64 + l;
+        w2h[f * 8 + i] = a;
+        w2h[(f + 64) * 8 + i] = b;
     } else if (tid < n1 + nb1 + n2 + nb2) {
-        const int i = tid - n1 - nb1 - n2;
-        const int l = i % 64, r = (i / 64) % 16, o = i / (64 * 16);
-        b2p[i] = B2(32 * o + hid(r, l >> 5));
+        const int q = tid - n1 - nb1 - n2;
+        const int l = q % 64, r = (q / 64) % 16, o = q / (64 * 16);
+        b2p[q] = B2(32 * o + hid(r, l >> 5));
     }
 }
 
@@ -217,7 +352,7 @@ extern "C" {
 int bgx_policy_packed_size(int32_t hidden, int32_t n_actions) {
     if (hidden <= 0 || hidden > 128 || n_actions <= 0) return BGX_EINVAL;
     const int T = (hidden + 31) / 32, OT = (n_actions + 1 + 31) / 32;
-    return kK1 * T * 64 + T * 16 * 64 + OT * 16 * T * 64 + OT * 16 * 64;
+    return kHdr + sz_w1q(T) + sz_b1p(T) + sz_w2q(T, OT) + sz_b2p(OT);
 }
 
 int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const float* ba, const float* wv, const float* bv,
@@ -225,12 +360,11 @@ int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const flo
     const int total = bgx_policy_packed_size(hidden, n_actions);
     if (total < 0 || !W1 || !b1 || !Wa || !ba || !wv || !bv || !packed) return BGX_EINVAL;
     const int T = (hidden + 31) / 32, OT = (n_actions + 1 + 31) / 32;
-    float* w1p = packed;
-    float* b1p = w1p + kK1 * T * 64;
-    float* w2p = b1p + T * 16 * 64;
-    float* b2p = w2p + OT * 16 * T * 64;
-    hipLaunchKernelGGL(k_policy_pack, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, W1, b1, Wa, ba, wv,
-                       bv, hidden, n_actions, T, OT, w1p, b1p, w2p, b2p);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_policy_scale, dim3(1), dim3(1024), 0, s, W1, Wa, wv, hidden, n_actions, packed);
+    const int work = kKB1 * T * 64 * 8 + T * 16 * 64 + OT * T * 2 * 64 * 8 + OT * 16 * 64;
+    hipLaunchKernelGGL(k_policy_pack, dim3((work + 255) / 256), dim3(256), 0, s, W1, b1, Wa, ba, wv, bv, hidden,
+                       n_actions, T, OT, packed);
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }
 
@@ -241,18 +375,14 @@ int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed, i
         return BGX_EINVAL;
     if (n == 0) return BGX_OK;
     const int T = (hidden + 31) / 32, OT = (n_actions + 1 + 31) / 32;
-    const float* w1p = packed;
-    const float* b1p = w1p + kK1 * T * 64;
-    const float* w2p = b1p + T * 16 * 64;
-    const float* b2p = w2p + OT * 16 * T * 64;
     const dim3 grid((n + 31) / 32), blk(64);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
     switch (T) {
-        case 1: hipLaunchKernelGGL(k_policy_act<1>, grid, blk, 0, s, records_dev, n, w1p, b1p, w2p, b2p, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
-        case 2: hipLaunchKernelGGL(k_policy_act<2>, grid, blk, 0, s, records_dev, n, w1p, b1p, w2p, b2p, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
-        case 3: hipLaunchKernelGGL(k_policy_act<3>, grid, blk, 0, s, records_dev, n, w1p, b1p, w2p, b2p, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
-        default: hipLaunchKernelGGL(k_policy_act<4>, grid, blk, 0, s, records_dev, n, w1p, b1p, w2p, b2p, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
+        case 1: hipLaunchKernelGGL(k_policy_act<1>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
+        case 2: hipLaunchKernelGGL(k_policy_act<2>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
+        case 3: hipLaunchKernelGGL(k_policy_act<3>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
+        default: hipLaunchKernelGGL(k_policy_act<4>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
     }
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }

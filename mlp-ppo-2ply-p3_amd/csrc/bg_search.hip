@@ -197,12 +197,12 @@ __device__ __forceinline__ bool two_ply_job(const Args& A, const SearchArgs& S, 
     for (int i = l; i < (1 << LOG); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const int r0 = kRoll0[r], r1 = kRoll1[r];
     if (r0 == r1)
-        for (int i = l; i < (2 << kLogMemo); i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = l; i < kMemoSlots; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     Gen<LOG, SlotPtr, MinSink<T>> g;
     g.tab = tab; g.pl = q; g.cap_unique = cap_unique;
     g.memo2 = r0 == r1 ? memo : nullptr;
-    g.memo3 = r0 == r1 ? memo + (1 << kLogMemo) : nullptr;
+    g.memo3 = r0 == r1 ? memo + (1 << kLogMemo2) : nullptr;
     g.sink.klist = klist; g.sink.ab = ab; g.sink.vn = vn; g.sink.q = q; g.sink.best = INFINITY;
     g.sink.evaluated = 0;
     uint32_t blk;
@@ -228,7 +228,7 @@ __device__ __forceinline__ bool two_ply_job(const Args& A, const SearchArgs& S, 
 template <int T>
 __global__ __launch_bounds__(64) void k_two_ply(Args A, SearchArgs S, VNet vn) {
     __shared__ uint4 tab[1 << kSearchLog];
-    __shared__ uint4 memo[2 << kLogMemo];
+    __shared__ uint4 memo[kMemoSlots];
     __shared__ uint4 klist[kKeyCap];
     __shared__ uint8_t ab[64];
     const int64_t njobs = (int64_t)(*S.rows_total) * 21;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(64) void k_two_ply(Args A, SearchArgs S, VNet vn) {
 
 template <int T>
 __global__ __launch_bounds__(64) void k_two_ply_slow(Args A, SearchArgs S, VNet vn, uint4* tables) {
-    __shared__ uint4 memo[2 << kLogMemo];
+    __shared__ uint4 memo[kMemoSlots];
     __shared__ uint4 klist[kKeyCap];
     __shared__ uint8_t ab[64];
     uint4* tab = tables + ((size_t)blockIdx.x << kLogSlotsSlow);

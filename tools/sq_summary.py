@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
             agg[k]["#" + r["Counter_Name"]] += 1
 for k, c in agg.items():
     w = c.get("SQ_WAVES", 0)
-    if not w or w < 1000:
+    if not w or w < float(os.environ.get("SQ_MIN_WAVES", "1000")):
         continue
     print(k)
     for n in sorted(x for x in c if not x.startswith("#")):

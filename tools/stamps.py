@@ -42,3 +42,23 @@ for k in range(0, bins, 2):
 # which blockIdx ranges run late
 late = np.argsort(-e)[:20]
 print("latest-ending lanes", late, dur[late] / 100, dbl[late])
+
+# slowest lanes over several steps: what are they? (saved for offline analysis)
+rows = []
+for k in range(12):
+    rec0 = eng.records()
+    pre = rec0.cpu().numpy()
+    a, _, _ = net.act(rec0, seed=1, step=2000 + k)
+    eng.step(a, want_obs=False, want_info=False)
+    assert L.bgx_debug_stamps(eng._h, st.ctypes.data_as(ctypes.c_void_p)) == 0
+    d = (st[:, 1] - st[:, 0]).astype(np.int64)
+    r2, _, nt = eng.lanes()
+    r2, nt = r2.cpu().numpy(), nt.cpu().numpy()
+    span = (st[:, 1].max() - st[:, 0].min()) / 100
+    for lane in np.argsort(-d)[:4]:
+        rows.append((k, lane, d[lane] / 100, span, r2[lane, 53], r2[lane, 54], nt[lane], r2[lane, 62] & 1, r2[lane].copy()))
+print("step lane dur_us span_us dice n_total ovf")
+for r in rows:
+    print(r[0], r[1], "%.1f %.1f" % (r[2], r[3]), r[4], r[5], r[6], r[7])
+np.savez(os.path.join(ROOT, "gpurun_out", "slow_lanes.npz"), recs=np.stack([r[8] for r in rows]),
+         dur=np.array([r[2] for r in rows]), ntot=np.array([r[6] for r in rows]))
