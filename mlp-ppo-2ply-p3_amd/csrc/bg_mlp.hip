@@ -127,7 +127,7 @@ __host__ __device__ inline void views(P base, int T, int OT, P& hdr, P& w1q, P& 
 }
 
 template <int T>
-__global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ recs, int n,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_policy_act(const uint8_t* __restrict__ recs, int n,
                                                    const float* __restrict__ packed, int n_actions, int n_otiles,
                                                    uint32_t seed_lo, uint32_t seed_hi, uint32_t step, int greedy,
                                                    int32_t* act_out, float* logp_out, float* value_out,
@@ -208,14 +208,10 @@ __global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ r
     const int grow = row0 + j;
     const uint32_t rowkey = mix32(mix32(seed_lo ^ mix32(seed_hi + 0x9E3779B9u)) ^ step) ^ (uint32_t)grow * 0x85EBCA6Bu;
     constexpr int NF = T * 2 * 2;                      // weight fragments per output tile
-    uint4 wcur[NF], wnxt[NF];
+    uint4 w[NF];
     #pragma unroll
-    for (int f = 0; f < NF; ++f) wcur[f] = w2q[(size_t)f * 64 + l];
+    for (int f = 0; f < NF; ++f) w[f] = w2q[(size_t)f * 64 + l];
     for (int o = 0; o < n_otiles; ++o) {
-        // prefetch the next tile's fragments behind this tile's MFMAs
-        const int on = o + 1 < n_otiles ? o + 1 : o;
-        #pragma unroll
-        for (int f = 0; f < NF; ++f) wnxt[f] = w2q[((size_t)on * NF + f) * 64 + l];
         f32x16 y;
         #pragma unroll
         for (int r = 0; r < 16; ++r) y[r] = b2p[(o * 16 + r) * 64 + l] * up;
@@ -223,14 +219,19 @@ __global__ __launch_bounds__(64) void k_policy_act(const uint8_t* __restrict__ r
         for (int t = 0; t < T; ++t)
             #pragma unroll
             for (int mm = 0; mm < 2; ++mm) {
-                const f16x8 ah = as_h8(wcur[(t * 2 + mm) * 2 + 0]);
-                const f16x8 al = as_h8(wcur[(t * 2 + mm) * 2 + 1]);
+                const f16x8 ah = as_h8(w[(t * 2 + mm) * 2 + 0]);
+                const f16x8 al = as_h8(w[(t * 2 + mm) * 2 + 1]);
                 y = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh[t][mm], y, 0, 0, 0);
                 y = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl[t][mm], y, 0, 0, 0);
                 y = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[t][mm], y, 0, 0, 0);
             }
-        #pragma unroll
-        for (int f = 0; f < NF; ++f) wcur[f] = wnxt[f];
+        // the next tile's fragments go into the same registers once this tile's
+        // MFMAs have issued; the loads overlap the sampling math below
+        __asm__ volatile("" ::: "memory");
+        if (o + 1 < n_otiles) {
+            #pragma unroll
+            for (int f = 0; f < NF; ++f) w[f] = w2q[((size_t)(o + 1) * NF + f) * 64 + l];
+        }
         // lane l holds outputs a = 32o + hid(r, h), r = 0..15, of row j
         float z[16];
         float tm = -INFINITY;
