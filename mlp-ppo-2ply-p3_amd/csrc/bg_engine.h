@@ -168,6 +168,9 @@ struct Args {
     // into cls; k_order turns the classes into perm (heaviest first) for the next launch.
     int32_t* perm;            // blockIdx -> lane, or null (identity)
     uint8_t* cls;             // [B] predicted cost class, or null
+    uint32_t* started;        // heavy launch: waves started so far (device memory), or null
+    uint32_t* gate;           // signal word set once the last heavy wave has started
+    uint32_t gate_n;          // heavy launch size
 };
 
 constexpr int kClasses = 4;
@@ -187,7 +190,9 @@ __device__ __forceinline__ int predict_class(int bv, uint64_t ctr, const Args& A
     const int off = nxt * 24;
     const bool mine = l >= off && l < off + 24 && bv > 0;
     const int pts = __popcll(__ballot(mine)) + (rd(bv, 48 + nxt) > 0 ? 2 : 0);
-    return pts >= 8 ? 0 : pts >= 6 ? 1 : 2;
+    // the slowest games are small doubles (1-1 .. 4-4) spread over many points
+    if ((a <= 2 && pts >= 7) || (a <= 4 && pts >= 9)) return 0;
+    return pts >= 6 ? 1 : 2;
 }
 
 // Enumerate the legal moves of (board in bv, player pl, roll) into `out`.
@@ -354,6 +359,11 @@ struct bgx_engine {
     int device;
     int lds_log;      // 9, 10 or 11
     int memo_mode;    // 1: separate memo tables, 2: memo inside the dedup table
+    bool split;       // Philox mode: doubles-prefix launch + light launch
+    hipStream_t side;     // light launch, gated on the heavy launch having started all its waves
+    hipEvent_t ev_fork, ev_join;
+    uint32_t* gate;       // signal memory: set when every heavy wave has started
+    uint32_t* started;    // device counter behind it
     bg::Args a;
     uint4* slow_tables;
     int slow_waves;

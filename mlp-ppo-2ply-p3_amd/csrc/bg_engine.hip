@@ -14,6 +14,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -38,6 +39,8 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
     uint4* memo = MEMO == 1 ? memo_ : MEMO == 2 ? tab : nullptr;
     const int bi = (int)blockIdx.x + base;
     const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : bi;
+    if (A.started && lane_id() == 0 && atomicAdd(A.started, 1u) == A.gate_n - 1u)
+        __hip_atomic_store(A.gate, A.gate_n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t t0 = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     // issue the independent loads together (record, action, dice counter)
     int bv = load_rec(A, gi);
@@ -385,18 +388,28 @@ static void launch_order(bgx_engine* e, hipStream_t s) {
 }
 
 static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, const int32_t* actions, float* obs,
-                        float* reward, uint8_t* done, int32_t* info) {
+                        float* reward, uint8_t* done, int32_t* info, int base = 0) {
+    if (grid <= 0) return;
     if (e->memo_mode == 2) {
         if (e->lds_log == 11)
-            hipLaunchKernelGGL((k_step<0, 11, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+            hipLaunchKernelGGL((k_step<0, 11, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
         else
-            hipLaunchKernelGGL((k_step<0, 10, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+            hipLaunchKernelGGL((k_step<0, 10, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
     } else if (e->lds_log == 9)
-        hipLaunchKernelGGL((k_step<0, 9>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+        hipLaunchKernelGGL((k_step<0, 9>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
     else if (e->lds_log == 11)
-        hipLaunchKernelGGL((k_step<0, 11>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+        hipLaunchKernelGGL((k_step<0, 11>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
     else
-        hipLaunchKernelGGL((k_step<0, 10>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, 0);
+        hipLaunchKernelGGL((k_step<0, 10>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
+}
+
+// Doubles share of the dispatch order (Philox mode): the expected doubles
+// fraction 1/6 plus 4 sigma.  Lanes past it run in the light launch whatever
+// their class (exact either way; an unpredicted doubles lane is only slower).
+static int heavy_grid(int B) {
+    const char* f = getenv("BGX_HEAVY_FRAC");
+    const double g = f ? atof(f) * B : B / 6.0 + 4.0 * std::sqrt(B * 5.0 / 36.0) + 32.0;
+    return g >= B ? B : (int)g;
 }
 
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
@@ -430,6 +443,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     const char* ll = getenv("BGX_LDS_LOG");
     e->lds_log = ll ? atoi(ll) : 10;
     if (e->lds_log < 9 || e->lds_log > 11) e->lds_log = 10;
+    const char* sp = getenv("BGX_SPLIT");
+    e->split = !(sp && sp[0] == '0');
     const char* mm = getenv("BGX_MEMO_MODE");
     e->memo_mode = mm ? atoi(mm) : 1;
     Args& A = e->a;
@@ -456,6 +471,11 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
         alloc((void**)&e->perm, B * 4);
         alloc((void**)&A.cls, B);
         alloc((void**)&e->order_cnt, (B / 1024 + 1) * kClasses * 4);
+        if (err == hipSuccess) err = hipExtMallocWithFlags((void**)&e->gate, 8, hipMallocSignalMemory);
+        alloc((void**)&e->started, 4);
+        if (err == hipSuccess) err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
+        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
     }
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }
     if (hipMemset(A.lanes, 0, B * 64) != hipSuccess || hipMemset(A.ctr, 0, B * 8) != hipSuccess ||
@@ -480,6 +500,11 @@ int bgx_engine_destroy(bgx_engine* e) {
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
                     e->slow_tables, e->search_ws, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
+    if (e->gate) (void)hipFree(e->gate);
+    if (e->started) (void)hipFree(e->started);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->side) (void)hipStreamDestroy(e->side);
     delete e;
     return BGX_OK;
 }
@@ -584,7 +609,35 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     } else {
         Args a = A;
         a.perm = e->perm_valid ? e->perm : nullptr;
-        launch_step(e, s, a, A.B, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+        if (a.perm && e->split) {
+            // two launches, in order: the predicted-doubles prefix with the big
+            // dedup table + revisit memo (26 KB of LDS per wave), then the rest
+            // with a 512-slot table and no memo (8 KB: ~3x the resident waves)
+            const int heavy = heavy_grid(A.B);
+            if (heavy < A.B) {
+                // the light launch waits (on a side stream) until every heavy wave
+                // has started, then fills the slots the heavy waves free: the
+                // doubles are never starved of LDS and their tail is covered
+                CK(hipMemsetAsync(e->gate, 0, 8, s));
+                CK(hipMemsetAsync(e->started, 0, 4, s));
+                CK(hipEventRecord(e->ev_fork, s));
+                CK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+                CK(hipStreamWaitValue32(e->side, e->gate, (uint32_t)heavy, hipStreamWaitValueGte, 0xFFFFFFFFu));
+                hipLaunchKernelGGL((k_step<0, 9, 0>), dim3(A.B - heavy), dim3(64), 0, e->side, a, actions_dev,
+                                   obs_dev, reward_dev, done_dev, info_dev, heavy);
+                Args ah = a;
+                ah.started = e->started;
+                ah.gate = e->gate;
+                ah.gate_n = (uint32_t)heavy;
+                launch_step(e, s, ah, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+                CK(hipEventRecord(e->ev_join, e->side));
+                CK(hipStreamWaitEvent(s, e->ev_join, 0));
+            } else {
+                launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+            }
+        } else {
+            launch_step(e, s, a, A.B, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+        }
         if (A.cls) launch_order(e, s);
     }
     CKL();

@@ -214,3 +214,42 @@ def test_large_batch_invariants(bgx):
     both = (rec[:, :24] > 0) & (rec[:, 24:48] > 0)
     assert not bool(both.any())
     assert eng.error() == 0
+
+
+def test_philox_split_dispatch_vs_oracle(bgx):
+    """Philox mode runs the predicted-doubles prefix of the dispatch order and the
+    light remainder (small table, no revisit memo) as separate launches: every
+    lane's move list and apply must still equal the oracle's, whichever launch
+    it ran in.  Each step: the oracle applies the chosen move to the previous
+    record, and the new record's move list is recomputed from its board/dice."""
+    B = 16384
+    eng = bgx.Engine(batch=B, max_moves=500, dice="philox", seed=9, auto_reset=True)
+    eng.reset()
+    g = torch.Generator(device="cuda").manual_seed(1)
+    checked_dbl = 0
+    for t in range(24):
+        prev, pmv, _ = eng.lanes()
+        prev, pmv = prev.cpu().numpy(), pmv.cpu().numpy().view(np.uint64)
+        nm = eng.n_moves()
+        a = (torch.rand(B, device="cuda", generator=g) * nm.clamp(min=1).float()).to(torch.int32)
+        eng.step(a, want_obs=False)
+        if t < 4 or t % 5:
+            continue
+        rec, mv, nt = eng.lanes()
+        rec, mv, nt = rec.cpu().numpy(), mv.cpu().numpy().view(np.uint64), nt.cpu().numpy()
+        a = a.cpu().numpy()
+        sel = np.arange(t, B, 11)
+        boards = np.ascontiguousarray(rec[sel, :52]).view(np.int8)
+        counts, ref = O.movegen_batch(boards, rec[sel, 52].copy(), rec[sel, 53:55].copy(), 500)
+        for k, i in enumerate(sel):
+            assert nt[i] == counts[k], (t, i)
+            n = min(int(counts[k]), 500)
+            assert np.array_equal(mv[i, :n], ref[k, :n]), (t, i)
+            checked_dbl += int(rec[i, 53] == rec[i, 54])
+            # the move applied this step, from the previous record (no game end, no pass)
+            if prev[i, 55] == 0 and (int(prev[i, 60]) | (int(prev[i, 61]) << 8)) > 0:
+                after = O.apply_move(prev[i, :52].view(np.int8), int(prev[i, 52]), int(pmv[i, a[i]]))
+                if after[50 + int(prev[i, 52])] < 15:
+                    assert np.array_equal(rec[i, :52].view(np.int8), after), (t, i)
+    assert checked_dbl > 500
+    assert eng.error() == 0
