@@ -256,16 +256,18 @@ def main():
     # record in+out 128, action 4, chosen move 8, new move list 8*n, reward 4, done 1, rng ctr 8+8
     bytes_per_lane = 128 + 4 + 8 + 8 * mean_moves + 4 + 1 + 16
     achieved = B * bytes_per_lane / (kern_ms * 1e-3) / 1e9
-    # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
+    # HBM bytes per env step (all kernels bgx_step launches: both k_step launches, the
+    # order sort, the overflow tiers) from the committed rocprofv3 PMC passes
     # (tools/profile.sh -> profiles/latest_summary.json; (2*FETCH_SIZE + WRITE_SIZE)*1024)
-    traffic, traffic_src = None, None
+    traffic, traffic_src, prof_kernels = None, None, None
     prof = os.path.join(ROOT, "profiles", "latest_summary.json")
     if os.path.exists(prof):
         try:
             summ = json.load(open(prof))
-            for k in summ["kernels"]:
-                if "k_step<0" in k["name"] and "hbm_bytes_per_launch" in k:
-                    traffic, traffic_src = k["hbm_bytes_per_launch"], summ.get("command")
+            env = summ.get("env_step")
+            if env and env["hbm_bytes_per_step"] > 0:
+                traffic, traffic_src = env["hbm_bytes_per_step"], summ.get("command")
+                prof_kernels = {k["name"]: round(k["avg_ns"] / 1e3, 1) for k in env["kernels"]}
         except Exception:
             traffic = None
     line = {
@@ -279,7 +281,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "int8 boards / bf16 policy MLP",
+        "dtype": "int8 boards / fp32-equivalent policy MLP (split-f16 MFMA)",
         "data": "synthetic self-play (Philox dice), random-init BackgammonPolicyNetwork weights",
         "burn_in": args.burn_in,
         "config": {"workload": (f"C3: B={B} games/GPU PPO rollout step (policy 198->128->{{500,1}} + masked "
@@ -287,11 +289,14 @@ def main():
                    f"C1-on-GPU: B={B} games/GPU random legal policy env.step",
                    "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
                    "parallelism": f"dp{ws} (independent game shards)"},
-        "roofline": {"kernel": "k_step<0> (apply + dice + move enumeration + dedup, one wave per game)",
+        "roofline": {"kernel": "env step: k_step<0,10,1> (doubles prefix) + k_step<0,9,0> (rest, gated side stream) "
+                               "+ k_order_count/scatter + k_movegen_over tiers; one wave per game; HIP events "
+                               "around bgx_step on the caller's stream (the side stream joins it)",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
-                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": B * bytes_per_lane,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/env step",
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_step": B * bytes_per_lane,
                      "kernel_ms": kern_ms, "bytes_per_lane_step": bytes_per_lane,
+                     "rocprof_avg_us": prof_kernels,
                      "mean_legal_moves": mean_moves},
     }
     if args.two_ply_batches > 0:

@@ -303,6 +303,7 @@ __device__ __forceinline__ Node rd_node(const Node& t, int src) {
 constexpr int kLogMemo2 = 7, kLogMemo3 = 9;
 constexpr int kMemoSlots = (1 << kLogMemo2) + (1 << kLogMemo3);    // memo2 = [0, 128), memo3 = [128, 640)
 constexpr int kMemoCap2 = (7 << kLogMemo2) / 8, kMemoCap3 = (7 << kLogMemo3) / 8;
+constexpr int kLogCMemo = 9;      // MEMO_KIND 1: depth-2 and depth-3 entries share one 512-slot table
 
 // Where surviving entries go.  MoveSink: the env's ordered move list in HBM
 // (first `cap` entries).  Other sinks (bg_search.hip) keep afterstate keys.
@@ -320,14 +321,16 @@ struct MoveSink {
     }
 };
 
-// TAGGED: the revisit memo lives in the dedup table itself under tagged keys
-// (hit-mask field complemented: >= 20 bits set, impossible for a real
+// MEMO_KIND: 0 = separate depth-2 / depth-3 memo tables; 1 = one combined memo
+// table; 2 = the memo lives in the dedup table itself.  Kinds 1-2 store tagged
+// keys (hit-mask field complemented: >= 20 bits set, impossible for a real
 // afterstate, which hits at most 4 blots; depth 3 also flips the bar nibble,
 // and bar + off + sum(counts) = 15 keeps the depth-2 and depth-3 images apart).
 constexpr uint32_t kTag2 = 0xFFFFFF00u, kTag3 = 0xFFFFFF0Fu;
 
-template <int LOG_SLOTS, typename SlotPtr, typename Sink = MoveSink, bool TAGGED = false>
+template <int LOG_SLOTS, typename SlotPtr, typename Sink = MoveSink, int MEMO_KIND = 0>
 struct Gen {
+    static constexpr bool TAGGED = MEMO_KIND == 2;
     SlotPtr tab;
     uint4* memo2;       // LDS memo tables (nullptr = no pruning)
     uint4* memo3;
@@ -468,23 +471,25 @@ struct Gen {
     template <int LOGM>
     __device__ __forceinline__ uint64_t memo_batch(uint4* memo, int& nm, bool act, const Node& t, uint32_t tag) {
         if (!memo) return __ballot(act);
-        constexpr int cap = (7 << LOGM) / 8;
+        constexpr int LOGT = MEMO_KIND == 1 ? kLogCMemo : LOGM;
         uint32_t slot = 0;
         bool found = true;
-        const uint32_t k3 = TAGGED ? t.k3 ^ tag : t.k3;
+        const uint32_t k3 = MEMO_KIND != 0 ? t.k3 ^ tag : t.k3;
         if (act) {
             if (TAGGED) found = probe_lane<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
-            else found = probe_lane<LOGM>(memo, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            else found = probe_lane<LOGT>(memo, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
         }
         const uint64_t fresh = __ballot(act && !found);
         uint64_t rec = fresh;
         int n = __popcll(rec);
-        int room = cap - nm;
-        if (TAGGED) room = min(room, cap_unique / 3 - n_memo2 - n_memo3);
+        int room;
+        if (MEMO_KIND == 0) room = ((7 << LOGM) / 8) - nm;
+        else if (MEMO_KIND == 1) room = ((7 << kLogCMemo) / 8) - n_memo2 - n_memo3;
+        else room = min(((7 << LOGM) / 8) - nm, cap_unique / 3 - n_memo2 - n_memo3);
         while (n > room && rec) { rec &= ~(1ull << (63 - __clzll((long long)rec))); --n; }
         if (rec) {
             if (TAGGED) place_batch<LOG_SLOTS, false>(tab, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
-            else place_batch<LOGM, false>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            else place_batch<LOGT, false>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
         }
         nm += n;
         return fresh;
@@ -571,6 +576,15 @@ struct Gen {
                 }
             }
         }
+    }
+
+    // non-doubles only (r0 != r1): the same as run() without the doubles code
+    __device__ __forceinline__ void run_nd(const Node& s0, int r0, int r1) {
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
+        const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
+        pass_nd(s0, hi, lo);
+        if (ovf) return;
+        if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi);   // :41-53
     }
 
     // get_all_possible_moves (get_all_moves.py:9-70)

@@ -168,12 +168,9 @@ struct Args {
     // into cls; k_order turns the classes into perm (heaviest first) for the next launch.
     int32_t* perm;            // blockIdx -> lane, or null (identity)
     uint8_t* cls;             // [B] predicted cost class, or null
-    uint32_t* started;        // heavy launch: waves started so far (device memory), or null
-    uint32_t* gate;           // signal word set once the last heavy wave has started
-    uint32_t gate_n;          // heavy launch size
 };
 
-constexpr int kClasses = 4;
+constexpr int kClasses = 5;
 
 // Cost class of the lane's NEXT movegen (0 = heaviest).  Philox dice are a pure
 // function of (key, lane, counter), so the next roll is known now; the mover
@@ -190,46 +187,51 @@ __device__ __forceinline__ int predict_class(int bv, uint64_t ctr, const Args& A
     const int off = nxt * 24;
     const bool mine = l >= off && l < off + 24 && bv > 0;
     const int pts = __popcll(__ballot(mine)) + (rd(bv, 48 + nxt) > 0 ? 2 : 0);
-    // the slowest games are small doubles (1-1 .. 4-4) spread over many points
-    if ((a <= 2 && pts >= 7) || (a <= 4 && pts >= 9)) return 0;
-    return pts >= 6 ? 1 : 2;
+    // tail risk of a doubles movegen grows with the points the mover occupies and
+    // falls with the die (tools/stamps.py table: p99 150-270 us at >= 9 points
+    // for 1-1 .. 4-4, ~60 us at 5 points): longest-first order
+    if (pts >= 10 && a <= 4) return 0;
+    if ((pts >= 8 && a <= 5) || pts >= 10) return 1;
+    return pts >= 5 ? 2 : 3;
 }
 
 // Enumerate the legal moves of (board in bv, player pl, roll) into `out`.
 // Returns n_moves (truncated); *total = untruncated count; *ovf on overflow.
-template <int LOG, typename SlotPtr, bool TAGGED = false>
+template <int LOG, typename SlotPtr, int MEMO_KIND = 0, bool NO_DOUBLES = false>
 __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint64_t* out, int cap, SlotPtr tab,
                                            int cap_unique, int* total, bool* ovf, uint4* memo) {
     constexpr int slots = 1 << LOG;
     for (int i = lane_id(); i < slots; i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = r0 == r1;
-    if (memo && dbl && !TAGGED)
-        for (int i = lane_id(); i < kMemoSlots; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (memo && dbl && MEMO_KIND != 2) {
+        constexpr int n = MEMO_KIND == 1 ? (1 << kLogCMemo) : kMemoSlots;
+        for (int i = lane_id(); i < n; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    Gen<LOG, SlotPtr, MoveSink, TAGGED> g;
+    Gen<LOG, SlotPtr, MoveSink, MEMO_KIND> g;
     g.tab = tab; g.sink.out = out; g.sink.cap = cap; g.pl = pl; g.cap_unique = cap_unique;
     g.memo2 = memo && dbl ? memo : nullptr;
-    g.memo3 = memo && dbl ? (TAGGED ? memo : memo + (1 << kLogMemo2)) : nullptr;
+    g.memo3 = memo && dbl ? (MEMO_KIND != 0 ? memo : memo + (1 << kLogMemo2)) : nullptr;
     uint32_t blocked;
     const Node s0 = node_from_bytes(bv, pl, blocked);
     g.blocked = blocked;
-    g.run(s0, r0, r1);
+    if (NO_DOUBLES) g.run_nd(s0, r0, r1);
+    else g.run(s0, r0, r1);
     *ovf = g.ovf;
     *total = g.count;
     return g.count < cap ? g.count : cap;
 }
 
-// Roll + movegen + obs for one lane according to its `need` byte
-// (reset: backgammon_env.py:78-113; pass/turn: :183-188 roll_dice + update_legal_moves).
-template <int LOG, bool TAGGED = false>
-__device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4* lds_tab, uint4* lds_memo,
-                                            uint64_t* ctr_io) {
+// Reset / dice part of advance_lane (reset: backgammon_env.py:78-113; pass/turn:
+// :183-188 roll_dice).  Returns false when the lane needs nothing this step.
+// mt_scratch: 624 words of LDS for the MT19937 twist (MT_LANE mode only).
+__device__ __forceinline__ bool roll_lane(int& bv, int gi, const Args& A, uint32_t* mt_scratch, uint64_t* ctr_io,
+                                          int& r0, int& r1) {
     const int need = rd(bv, R_NEED);
-    if (need == NEED_NONE) return bv;
+    if (need == NEED_NONE) return false;
     Rng rng;
     if (A.dice_mode == BGX_DICE_PHILOX) rng.init_philox(*ctr_io, A.key0, A.key1, (uint32_t)gi);
-    else if (A.dice_mode == BGX_DICE_MT_LANE) rng.init_mt(A.mt + (size_t)gi * kMtWords, (uint32_t*)lds_tab);
-    int r0, r1;
+    else if (A.dice_mode == BGX_DICE_MT_LANE) rng.init_mt(A.mt + (size_t)gi * kMtWords, mt_scratch);
     if (need == NEED_RESET) {
         if (rd(bv, R_MATCH)) { bv = wr(bv, R_S0, 0); bv = wr(bv, R_S1, 0); bv = wr(bv, R_MATCH, 0); }
         if (lane_id() < 52) bv = initial_byte(lane_id());
@@ -257,11 +259,21 @@ __device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4
     if (A.dice_mode == BGX_DICE_PHILOX) *ctr_io = rng.ctr;
     bv = wr(bv, R_ROLL0, r0);
     bv = wr(bv, R_ROLL1, r1);
+    return true;
+}
+
+// update_legal_moves (backgammon_env.py:193-231) for the rolled dice: move list,
+// counts and flags into the record / HBM; overflowed lanes are queued for the
+// bigger tables.
+template <int LOG, int MEMO_KIND, bool NO_DOUBLES = false>
+__device__ __forceinline__ int movegen_lane(int bv, int gi, const Args& A, int r0, int r1, uint4* lds_tab,
+                                            uint4* lds_memo) {
     const int cur = rd(bv, R_CUR);
     int total;
     bool ovf;
-    int n = run_movegen<LOG, uint4*, TAGGED>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves, A.max_moves, lds_tab,
-                             cap_fast<LOG>(), &total, &ovf, lds_memo);
+    int n = run_movegen<LOG, uint4*, MEMO_KIND, NO_DOUBLES>(bv, cur, r0, r1, A.moves + (size_t)gi * A.max_moves,
+                                                             A.max_moves, lds_tab, cap_fast<LOG>(), &total, &ovf,
+                                                             lds_memo);
     int flags = rd(bv, R_FLAGS) & ~1;
     if (ovf) {
         if (lane_id() == 0) { const int q = atomicAdd(A.ovf_count, 1); A.ovf_queue[q] = gi; }
@@ -273,6 +285,27 @@ __device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4
     bv = wr(bv, R_FLAGS, flags);
     bv = wr(bv, R_NEED, NEED_NONE);
     return bv;
+}
+
+// Hand the lane to the overflow tiers (k_movegen_over) instead of enumerating here.
+__device__ __forceinline__ int defer_lane(int bv, int gi, const Args& A) {
+    if (lane_id() == 0) { const int q = atomicAdd(A.ovf_count, 1); A.ovf_queue[q] = gi; A.n_total[gi] = 0; }
+    bv = wr(bv, R_NM0, 0);
+    bv = wr(bv, R_NM1, 0);
+    bv = wr(bv, R_FLAGS, rd(bv, R_FLAGS) | 1);
+    return wr(bv, R_NEED, NEED_NONE);
+}
+
+// Roll + movegen for one lane according to its `need` byte.  NO_DOUBLES (the
+// light launch of the split dispatch): a doubles roll goes to the overflow tiers,
+// so this instantiation carries only the non-doubles enumeration (registers).
+template <int LOG, int MEMO_KIND = 0, bool NO_DOUBLES = false>
+__device__ __forceinline__ int advance_lane(int bv, int gi, const Args& A, uint4* lds_tab, uint4* lds_memo,
+                                            uint64_t* ctr_io) {
+    int r0, r1;
+    if (!roll_lane(bv, gi, A, (uint32_t*)lds_tab, ctr_io, r0, r1)) return bv;
+    if (NO_DOUBLES && r0 == r1) return defer_lane(bv, gi, A);
+    return movegen_lane<LOG, MEMO_KIND, NO_DOUBLES>(bv, gi, A, r0, r1, lds_tab, lds_memo);
 }
 
 __device__ __forceinline__ void write_obs(int bv, float* obs_row) {
@@ -359,11 +392,7 @@ struct bgx_engine {
     int device;
     int lds_log;      // 9, 10 or 11
     int memo_mode;    // 1: separate memo tables, 2: memo inside the dedup table
-    bool split;       // Philox mode: doubles-prefix launch + light launch
-    hipStream_t side;     // light launch, gated on the heavy launch having started all its waves
-    hipEvent_t ev_fork, ev_join;
-    uint32_t* gate;       // signal memory: set when every heavy wave has started
-    uint32_t* started;    // device counter behind it
+    bool split;       // Philox mode: doubles-prefix launch, then the light launch
     bg::Args a;
     uint4* slow_tables;
     int slow_waves;

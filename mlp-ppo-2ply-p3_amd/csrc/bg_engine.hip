@@ -28,19 +28,11 @@ using namespace bg;
 
 // -------------------------------------------------------------- kernels --
 // PHASE 0: apply + advance fused (per-lane dice); 1: apply only; 2: advance only.
-// `base` offsets blockIdx into the dispatch order.  MEMO: 0 = no revisit memo,
-// 1 = separate memo tables (8 KB of LDS), 2 = memo inside the dedup table
-// (tagged keys; 16 KB per wave in all).
-template <int PHASE, int LOG, int MEMO = 1>
-__global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
-                                             int32_t* info, int base) {
-    __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo_[MEMO == 1 ? kMemoSlots : 1];
-    uint4* memo = MEMO == 1 ? memo_ : MEMO == 2 ? tab : nullptr;
-    const int bi = (int)blockIdx.x + base;
-    const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : bi;
-    if (A.started && lane_id() == 0 && atomicAdd(A.started, 1u) == A.gate_n - 1u)
-        __hip_atomic_store(A.gate, A.gate_n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// One lane's step: apply (PHASE 0/1), roll + movegen (PHASE 0/2), record, next
+// dispatch class.
+template <int PHASE, int LOG, int MEMO, bool NO_DOUBLES = false>
+__device__ __forceinline__ void step_lane(const Args& A, int gi, uint4* tab, uint4* memo, const int32_t* actions,
+                                          float* obs, float* reward, uint8_t* done, int32_t* info) {
     const uint64_t t0 = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     // issue the independent loads together (record, action, dice counter)
     int bv = load_rec(A, gi);
@@ -48,7 +40,7 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
     uint64_t ctr = A.dice_mode == BGX_DICE_PHILOX ? A.ctr[gi] : 0;
     if (PHASE != 2) bv = apply_lane(bv, gi, act, A, reward, done, info);
     if (PHASE != 1) {
-        bv = advance_lane<LOG, MEMO == 2>(bv, gi, A, tab, memo, &ctr);
+        bv = advance_lane<LOG, MEMO == 2 ? 2 : 0, NO_DOUBLES>(bv, gi, A, tab, memo, &ctr);
         if (obs) write_obs(bv, obs + (size_t)gi * 198);
     }
     store_rec(A, gi, bv);
@@ -60,6 +52,20 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
         A.stamps[2 * gi] = t0;
         A.stamps[2 * gi + 1] = __builtin_amdgcn_s_memrealtime();
     }
+}
+
+// `base` offsets blockIdx into the dispatch order.  MEMO: 0 = no revisit memo,
+// 1 = separate memo tables (10 KB of LDS), 2 = memo inside the dedup table.
+// NO_DOUBLES: doubles rolls are deferred to the overflow tiers (light launch).
+template <int PHASE, int LOG, int MEMO = 1, bool NO_DOUBLES = false>
+__global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
+                                             int32_t* info, int base) {
+    __shared__ uint4 tab[1 << LOG];
+    __shared__ uint4 memo_[MEMO == 1 ? kMemoSlots : 1];
+    uint4* memo = MEMO == 1 ? memo_ : MEMO == 2 ? tab : nullptr;
+    const int bi = (int)blockIdx.x + base;
+    const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : bi;
+    step_lane<PHASE, LOG, MEMO, NO_DOUBLES>(A, gi, tab, memo, actions, obs, reward, done, info);
 }
 
 template <int LOG>
@@ -471,11 +477,6 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
         alloc((void**)&e->perm, B * 4);
         alloc((void**)&A.cls, B);
         alloc((void**)&e->order_cnt, (B / 1024 + 1) * kClasses * 4);
-        if (err == hipSuccess) err = hipExtMallocWithFlags((void**)&e->gate, 8, hipMallocSignalMemory);
-        alloc((void**)&e->started, 4);
-        if (err == hipSuccess) err = hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking);
-        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
-        if (err == hipSuccess) err = hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming);
     }
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }
     if (hipMemset(A.lanes, 0, B * 64) != hipSuccess || hipMemset(A.ctr, 0, B * 8) != hipSuccess ||
@@ -500,11 +501,6 @@ int bgx_engine_destroy(bgx_engine* e) {
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
                     e->slow_tables, e->search_ws, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
-    if (e->gate) (void)hipFree(e->gate);
-    if (e->started) (void)hipFree(e->started);
-    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
-    if (e->side) (void)hipStreamDestroy(e->side);
     delete e;
     return BGX_OK;
 }
@@ -609,35 +605,17 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     } else {
         Args a = A;
         a.perm = e->perm_valid ? e->perm : nullptr;
-        if (a.perm && e->split) {
-            // two launches, in order: the predicted-doubles prefix with the big
-            // dedup table + revisit memo (26 KB of LDS per wave), then the rest
-            // with a 512-slot table and no memo (8 KB: ~3x the resident waves)
-            const int heavy = heavy_grid(A.B);
-            if (heavy < A.B) {
-                // the light launch waits (on a side stream) until every heavy wave
-                // has started, then fills the slots the heavy waves free: the
-                // doubles are never starved of LDS and their tail is covered
-                CK(hipMemsetAsync(e->gate, 0, 8, s));
-                CK(hipMemsetAsync(e->started, 0, 4, s));
-                CK(hipEventRecord(e->ev_fork, s));
-                CK(hipStreamWaitEvent(e->side, e->ev_fork, 0));
-                CK(hipStreamWaitValue32(e->side, e->gate, (uint32_t)heavy, hipStreamWaitValueGte, 0xFFFFFFFFu));
-                hipLaunchKernelGGL((k_step<0, 9, 0>), dim3(A.B - heavy), dim3(64), 0, e->side, a, actions_dev,
-                                   obs_dev, reward_dev, done_dev, info_dev, heavy);
-                Args ah = a;
-                ah.started = e->started;
-                ah.gate = e->gate;
-                ah.gate_n = (uint32_t)heavy;
-                launch_step(e, s, ah, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
-                CK(hipEventRecord(e->ev_join, e->side));
-                CK(hipStreamWaitEvent(s, e->ev_join, 0));
-            } else {
-                launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
-            }
-        } else {
-            launch_step(e, s, a, A.B, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
-        }
+        const int heavy = a.perm && e->split ? heavy_grid(A.B) : A.B;
+        // Split dispatch (Philox mode): the predicted-doubles prefix of the order
+        // with the big dedup table + revisit memo (26 KB of LDS per wave), then the
+        // rest with a 256-slot table, no memo, no doubles code (4 KB, 49 VGPRs: the
+        // hardware wave limit, ~5x the resident waves; doubles go to the overflow tiers).
+        // Plain stream order -- no cross-stream wait that a serializing tool
+        // (profiler) or a shared hardware queue could deadlock.
+        launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+        if (heavy < A.B)
+            hipLaunchKernelGGL((k_step<0, 8, 0, true>), dim3(A.B - heavy), dim3(64), 0, s, a, actions_dev, obs_dev,
+                               reward_dev, done_dev, info_dev, heavy);
         if (A.cls) launch_order(e, s);
     }
     CKL();

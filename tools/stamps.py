@@ -62,3 +62,27 @@ for r in rows:
     print(r[0], r[1], "%.1f %.1f" % (r[2], r[3]), r[4], r[5], r[6], r[7])
 np.savez(os.path.join(ROOT, "gpurun_out", "slow_lanes.npz"), recs=np.stack([r[8] for r in rows]),
          dur=np.array([r[2] for r in rows]), ntot=np.array([r[6] for r in rows]))
+
+# doubles cost table by (die, points occupied by the mover + 2*on-bar) over several steps
+tab = {}
+for k in range(8):
+    rec0 = eng.records()
+    a, _, _ = net.act(rec0, seed=1, step=3000 + k)
+    eng.step(a, want_obs=False, want_info=False)
+    assert L.bgx_debug_stamps(eng._h, st.ctypes.data_as(ctypes.c_void_p)) == 0
+    d = (st[:, 1] - st[:, 0]).astype(np.int64) / 100.0
+    r = eng.records().cpu().numpy()
+    cur = r[:, 52].astype(np.int64)
+    bd = r[:, :48].view(np.int8).reshape(B, 2, 24)
+    pts = (bd[np.arange(B), cur] > 0).sum(1) + 2 * (r[np.arange(B), 48 + cur] > 0)
+    dbl = r[:, 53] == r[:, 54]
+    for i in np.nonzero(dbl)[0]:
+        tab.setdefault((int(r[i, 53]), int(pts[i])), []).append(d[i])
+print("die pts: n mean p90 p99 (us)")
+for die in range(1, 7):
+    row = []
+    for p in range(0, 16):
+        v = tab.get((die, p))
+        if v and len(v) >= 20:
+            row.append("%2d:%5.0f/%4.0f" % (p, np.mean(v), np.percentile(v, 99)))
+    print(die, " ".join(row))

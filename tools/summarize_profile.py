@@ -9,6 +9,7 @@ import statistics
 import sys
 
 out, cmd = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "")
+pmc_cmd = sys.argv[3] if len(sys.argv) > 3 else cmd
 stats = list(csv.DictReader(open(os.path.join(out, "trace", "run_kernel_stats.csv"))))
 
 
@@ -25,7 +26,7 @@ def pmc(kind, counter):
 
 fetch, write = pmc("fetch", "FETCH_SIZE"), pmc("write", "WRITE_SIZE")
 kernels = []
-for s in stats[:12]:
+for s in stats[:16]:
     name = s["Name"]
     k = {"name": name, "calls": int(s["Calls"]), "avg_ns": float(s["AverageNs"]), "pct": float(s["Percentage"])}
     f = next((v for n, v in fetch.items() if n == name), None)
@@ -47,7 +48,19 @@ for k in kernels[:4]:
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in trace if r["Kernel_Name"] == k["name"]]
     if tail and len(d) >= tail:
         k["avg_ns_timed_tail"] = statistics.mean(d[-tail:])
-summary = {"command": "python bench.py " + cmd, "kernels": kernels}
+# the env step = every kernel bgx_step launches once per step (Philox split dispatch):
+# both k_step launches, the dispatch-order sort, and the overflow tiers
+STEP_KERNELS = ("k_step<0", "k_order_count", "k_order_scatter", "k_movegen_over<0")
+env = {"kernels": [], "hbm_bytes_per_step": 0.0, "busy_ns_per_step": 0.0}
+for k in kernels:
+    short = k["name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    if any(short.startswith(p) for p in STEP_KERNELS):
+        env["kernels"].append({"name": short.split("(")[0], "avg_ns": k["avg_ns"],
+                               "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch")})
+        env["busy_ns_per_step"] += k["avg_ns"]
+        env["hbm_bytes_per_step"] += k.get("hbm_bytes_per_launch") or 0.0
+summary = {"command": "python bench.py " + cmd, "pmc_command": "python bench.py " + pmc_cmd,
+           "kernels": kernels, "env_step": env}
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
 for k in kernels:
     print(f"{k['pct']:6.2f}% {k['avg_ns']/1e3:10.1f} us (tail {k.get('avg_ns_timed_tail', 0)/1e3:.1f}) "
