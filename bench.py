@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--two-ply-batches", type=int, default=1,
                     help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
     ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--shards", type=int, default=1,
+                    help="the B games of a GPU as S engines of B/S lanes on S streams (measured: S=2 -4%%, "
+                         "S=4 -46%% vs S=1 on MI355X; kept for experiments)")
     ap.add_argument("--burn-in", type=int, default=150,
                     help="untimed steps before warmup so the game population reaches its steady mix "
                          "(openings are cheaper than mid-game positions)")
@@ -175,59 +178,75 @@ def main():
     from bgx.policy import PolicyNet
 
     B = args.batch
-    eng = bgx.Engine(batch=B, max_moves=500, seed=1234 + 7919 * rank, dice="philox", auto_reset=True, device=dev)
-    eng.reset(want_obs=True)
+    S = max(1, args.shards)
+    assert B % S == 0
+    Bs = B // S
+    engs = [bgx.Engine(batch=Bs, max_moves=500, seed=1234 + 7919 * rank + 104729 * k, dice="philox", auto_reset=True,
+                       device=dev) for k in range(S)]
+    for e in engs:
+        e.reset(want_obs=True)
+    eng = engs[0]
     torch.manual_seed(0)
     net = PolicyNet(hidden_size=128, action_size=500).to(dev)
     net.pack()
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     ring = 8
-    pin = {
-        "boards": torch.empty(ring, B, 64, dtype=torch.uint8).pin_memory(),
-        "act": torch.empty(ring, B, dtype=torch.int32).pin_memory(),
-        "logp": torch.empty(ring, B, dtype=torch.float32).pin_memory(),
-        "value": torch.empty(ring, B, dtype=torch.float32).pin_memory(),
-        "reward": torch.empty(ring, B, dtype=torch.float32).pin_memory(),
-        "done": torch.empty(ring, B, dtype=torch.uint8).pin_memory(),
-    }
-    copy_stream = torch.cuda.Stream(dev)
-    counts = torch.empty(B, dtype=torch.int16, device=dev)
+    pins = [{
+        "boards": torch.empty(ring, Bs, 64, dtype=torch.uint8).pin_memory(),
+        "act": torch.empty(ring, Bs, dtype=torch.int32).pin_memory(),
+        "logp": torch.empty(ring, Bs, dtype=torch.float32).pin_memory(),
+        "value": torch.empty(ring, Bs, dtype=torch.float32).pin_memory(),
+        "reward": torch.empty(ring, Bs, dtype=torch.float32).pin_memory(),
+        "done": torch.empty(ring, Bs, dtype=torch.uint8).pin_memory(),
+    } for _ in range(S)]
+    copy_streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    counts = [torch.empty(Bs, dtype=torch.int16, device=dev) for _ in range(S)]
     gen = torch.Generator(device=dev).manual_seed(99 + rank)
     ev_pairs = []
     state = {"i": 0}
 
+    def shard_step(k, i, timed):
+        e, st = engs[k], streams[k]
+        with torch.cuda.stream(st):
+            if args.workload == "c1":
+                e.n_moves(out=counts[k])
+                act = (torch.rand(Bs, device=dev, generator=gen) * counts[k].clamp(min=1).float()).to(torch.int32)
+                if timed:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                e.step(act, want_obs=False, want_info=False)
+                if timed:
+                    e1.record(st)
+                    ev_pairs.append((e0, e1))
+                return
+            rec = net.rollout_inputs(e)                         # int8 lane boards (no fp32 obs round trip)
+            act, logp, value = net.act(rec, seed=4242 + rank * 16 + k, step=i)   # fused HIP policy step
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+            _, rew, done, _ = e.step(act, want_obs=False, want_info=False)
+            if timed:
+                e1.record(st)
+                ev_pairs.append((e0, e1))
+            # rollout record -> pinned host ring (side stream, overlapped)
+            slot = i % ring
+            cs = copy_streams[k]
+            cs.wait_stream(st)
+            with torch.cuda.stream(cs):
+                for name, v in (("boards", rec), ("act", act), ("logp", logp), ("value", value),
+                                ("reward", rew), ("done", done)):
+                    pins[k][name][slot].copy_(v, non_blocking=True)
+                    v.record_stream(cs)
+            st.wait_stream(cs) if slot == ring - 1 else None
+
     def step(timed: bool):
         i = state["i"]
         state["i"] += 1
-        if args.workload == "c1":
-            eng.n_moves(out=counts)
-            act = (torch.rand(B, device=dev, generator=gen) * counts.clamp(min=1).float()).to(torch.int32)
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            eng.step(act, want_obs=False, want_info=False)
-            if timed:
-                e1.record()
-                ev_pairs.append((e0, e1))
-            return
-        rec = net.rollout_inputs(eng)                       # int8 lane boards (no fp32 obs round trip)
-        act, logp, value = net.act(rec, seed=4242 + rank, step=i)   # fused HIP policy step
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        _, rew, done, _ = eng.step(act, want_obs=False, want_info=False)
-        if timed:
-            e1.record()
-            ev_pairs.append((e0, e1))
-        # rollout record -> pinned host ring (side stream, overlapped)
-        slot = i % ring
-        cur = torch.cuda.current_stream(dev)
-        copy_stream.wait_stream(cur)
-        with torch.cuda.stream(copy_stream):
-            for k, v in (("boards", rec), ("act", act), ("logp", logp), ("value", value),
-                         ("reward", rew), ("done", done)):
-                pin[k][slot].copy_(v, non_blocking=True)
-                v.record_stream(copy_stream)
-        cur.wait_stream(copy_stream) if slot == ring - 1 else None
+        for k in range(S):
+            shard_step(k, i, timed)
+
+    def sync_all():
+        torch.cuda.synchronize(dev)
 
     for _ in range(args.burn_in):
         step(False)
@@ -236,7 +255,8 @@ def main():
     for w in range(args.warmup):
         step(False)
         if w >= args.warmup // 2:
-            nm_sum += float(eng.n_moves(out=counts).float().mean().item())
+            sync_all()
+            nm_sum += sum(float(e.n_moves(out=counts[k]).float().mean().item()) for k, e in enumerate(engs)) / S
             nm_n += 1
     mean_moves = nm_sum / max(nm_n, 1)
     torch.cuda.synchronize(dev)
@@ -255,7 +275,7 @@ def main():
     # algorithmic bytes per lane-step of the env-step kernel:
     # record in+out 128, action 4, chosen move 8, new move list 8*n, reward 4, done 1, rng ctr 8+8
     bytes_per_lane = 128 + 4 + 8 + 8 * mean_moves + 4 + 1 + 16
-    achieved = B * bytes_per_lane / (kern_ms * 1e-3) / 1e9
+    achieved = Bs * bytes_per_lane / (kern_ms * 1e-3) / 1e9    # one shard's env step per window
     # HBM bytes per env step (all kernels bgx_step launches: both k_step launches, the
     # order sort, the overflow tiers) from the committed rocprofv3 PMC passes
     # (tools/profile.sh -> profiles/latest_summary.json; (2*FETCH_SIZE + WRITE_SIZE)*1024)
@@ -288,19 +308,27 @@ def main():
                                 "sample + env.step)") if args.workload == "c3" else
                    f"C1-on-GPU: B={B} games/GPU random legal policy env.step",
                    "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
-                   "parallelism": f"dp{ws} (independent game shards)"},
-        "roofline": {"kernel": "env step: k_step<0,10,1> (doubles prefix) + k_step<0,9,0> (rest, gated side stream) "
-                               "+ k_order_count/scatter + k_movegen_over tiers; one wave per game; HIP events "
-                               "around bgx_step on the caller's stream (the side stream joins it)",
+                   "parallelism": f"dp{ws} (independent game shards)", "shards_per_gpu": S,
+                   "streams_per_gpu": S},
+        "roofline": {"kernel": "env step = k_step<0,10,1> (predicted-doubles prefix) then k_step<0,8,0,true> "
+                               "(the rest) + k_order_count/scatter + k_movegen_over tiers, one wave per game, "
+                               "all on the caller's stream; HIP events around bgx_step",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/env step",
-                     "traffic_source": traffic_src, "algorithmic_bytes_per_step": B * bytes_per_lane,
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_step": Bs * bytes_per_lane, "lanes_per_launch": Bs,
                      "kernel_ms": kern_ms, "bytes_per_lane_step": bytes_per_lane,
                      "rocprof_avg_us": prof_kernels,
                      "mean_legal_moves": mean_moves},
     }
     if args.two_ply_batches > 0:
-        line["two_ply"] = two_ply_bench(eng, args.two_ply_batches, ws, dev)
+        eng2 = engs[0] if S == 1 else bgx.Engine(batch=B, max_moves=500, seed=77 + rank, dice="philox",
+                                                 auto_reset=True, device=dev)
+        if S > 1:                                  # full-batch positions for C4: a short self-play burn-in
+            eng2.reset(want_obs=False)
+            for i in range(60):
+                a2, _, _ = net.act(net.rollout_inputs(eng2), seed=5, step=i)
+                eng2.step(a2, want_obs=False, want_info=False)
+        line["two_ply"] = two_ply_bench(eng2, args.two_ply_batches, ws, dev)
     if args.horizon > 0 and args.workload in ("c3", "ppo"):
         line["ppo_iteration"] = ppo_iteration_bench(B, args.horizon, ws, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:

@@ -26,7 +26,7 @@ def pmc(kind, counter):
 
 fetch, write = pmc("fetch", "FETCH_SIZE"), pmc("write", "WRITE_SIZE")
 kernels = []
-for s in stats[:16]:
+for s in stats:
     name = s["Name"]
     k = {"name": name, "calls": int(s["Calls"]), "avg_ns": float(s["AverageNs"]), "pct": float(s["Percentage"])}
     f = next((v for n, v in fetch.items() if n == name), None)
@@ -60,8 +60,8 @@ for k in kernels:
         env["busy_ns_per_step"] += k["avg_ns"]
         env["hbm_bytes_per_step"] += k.get("hbm_bytes_per_launch") or 0.0
 summary = {"command": "python bench.py " + cmd, "pmc_command": "python bench.py " + pmc_cmd,
-           "kernels": kernels, "env_step": env}
+           "kernels": kernels[:20], "env_step": env}
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
-for k in kernels:
+for k in kernels[:20]:
     print(f"{k['pct']:6.2f}% {k['avg_ns']/1e3:10.1f} us (tail {k.get('avg_ns_timed_tail', 0)/1e3:.1f}) "
           f"x{k['calls']:4d}  {k['name'][:70]}  {k.get('hbm_bytes_per_launch', 0)/1e6:.1f} MB")
