@@ -272,6 +272,33 @@ __device__ __forceinline__ int lane_rank(uint64_t m) {          // set bits of m
     return __popcll(m & ((1ull << lane) - 1ull));
 }
 
+// position of the j-th (0-based) set bit of m (j < popcount(m)), per lane
+__device__ __forceinline__ int select_bit(uint32_t m, int j) {
+    int pos = 0;
+    #pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        const int c = __popc(m & ((1u << w) - 1u));
+        const bool up = j >= c;
+        j -= up ? c : 0;
+        m = up ? m >> w : m;
+        pos += up ? w : 0;
+    }
+    return pos;
+}
+
+// lane `src`'s Node (per-lane source index: ds_bpermute)
+__device__ __forceinline__ Node shfl_node(const Node& t, int src) {
+    Node s;
+    s.lo = (uint64_t)(uint32_t)__shfl((int)(uint32_t)t.lo, src) |
+           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(t.lo >> 32), src) << 32);
+    s.hi = (uint32_t)__shfl((int)t.hi, src);
+    s.k3 = (uint32_t)__shfl((int)t.k3, src);
+    s.occ = (uint32_t)__shfl((int)t.occ, src);
+    s.blot = (uint32_t)__shfl((int)t.blot, src);
+    s.n_home = __shfl(t.n_home, src);
+    return s;
+}
+
 __device__ __forceinline__ Node rd_node(const Node& t, int src) {
     Node s;
     s.lo = (uint64_t)rdl((uint32_t)t.lo, src) | ((uint64_t)rdl((uint32_t)(t.lo >> 32), src) << 32);
@@ -401,46 +428,56 @@ struct Gen {
         commit(__ballot(act && !found), t, enc, slot, len);
     }
 
-    // Leaves of two nodes in one batch: lanes 0..31 = child bit l of node A,
-    // lanes 32..63 = child bit l-32 of node B (bit 31 = the special move), so
-    // lane order is child order, A before B.  Cousins may coincide: DEDUP commit.
-    __device__ __forceinline__ void pair_batch(const Node& sA, const Kids& kA, uint64_t pA, const Node& sB,
-                                               const Kids& kB, uint64_t pB, int d, int shift, int len) {
+    // All children of the parent nodes on the lanes in `parents` (lane = the
+    // parent's child bit, so lane order is DFS order), flattened into 64-lane
+    // chunks: leaf p of the chunk belongs to the parent whose prefix range holds
+    // it and is that parent's (p - prefix)-th child.  Entries are
+    // penc | enc << shift of length len.  Cousins may coincide: DEDUP commit.
+    __device__ __forceinline__ void flat_leaves(uint64_t parents, const Node& t, uint32_t q, int x, uint64_t penc,
+                                                int d, int shift, int len) {
         const int l = threadIdx.x & 63;
-        const bool hb = l >= 32;
-        const int bit = l & 31;
-        const uint32_t bits = hb ? kB.bits : kA.bits;
-        const bool act = (bits >> bit) & 1u;
-        Node t;
-        uint64_t enc = 0;
-        if (act) {
-            const Node& s = hb ? sB : sA;
-            const Kids k{bits, hb ? kB.extra : kA.extra};
-            const Sub m = child(s, k, bit, d, pl);
-            t = apply(s, m, pl);
-            enc = (hb ? pB : pA) | ((uint64_t)m.enc << shift);
+        const bool par = (parents >> l) & 1ull;
+        const uint32_t cnt = par ? (uint32_t)__popc(q) : 0u;         // <= 25
+        uint32_t pre = 0, total = 0;
+        const uint64_t below = (1ull << l) - 1ull;
+        #pragma unroll
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t m = __ballot((cnt >> b) & 1u);
+            pre += (uint32_t)__popcll(m & below) << b;
+            total += (uint32_t)__popcll(m) << b;
         }
+        const uint64_t live = __ballot(cnt != 0u);
         BG_CNT(6, 1);
-        BG_CNT(7, __popc(kA.bits) + __popc(kB.bits));
-        BG_T0(tp);
-        uint32_t slot = 0;
-        bool found = true;
-        if (act) found = probe_lane<LOG_SLOTS>(tab, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
-        commit<true>(__ballot(act && !found), t, enc, slot, len);
-        BG_T1(14, tp);
-    }
-
-    // All children of s as entries prefix | enc << shift of length len.
-    __device__ __forceinline__ void leaf_batch(const Node& s, const Kids& k, int d, uint64_t prefix, int shift,
-                                               int len) {
-        Node t;
-        uint32_t e = 0;
-        const bool act = lane_child(s, k, d, t, e);
-        BG_CNT(6, 1);
-        BG_CNT(7, __popc(k.bits));
-        BG_T0(tp);
-        batch(act, t, prefix | ((uint64_t)e << shift), len);
-        BG_T1(14, tp);
+        BG_CNT(7, total);
+        for (uint32_t c = 0; c < total; c += 64) {
+            const uint32_t pp = c + (uint32_t)l;
+            const bool valid = pp < total;
+            int src = 0;
+            for (uint64_t m = live; m; m &= m - 1ull) {
+                const int i = __ffsll((unsigned long long)m) - 1;
+                const uint32_t pi = rdl(pre, i);
+                if (pi >= c + 64u) break;
+                src = pp >= pi ? i : src;
+            }
+            const uint32_t qb = (uint32_t)__shfl((int)q, src);
+            const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
+            const Node s = shfl_node(t, src);
+            const Kids k{qb, __shfl(x, src)};
+            const uint64_t pe = (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc, src) |
+                                ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(penc >> 32), src) << 32);
+            Node leaf;
+            uint64_t enc = 0;
+            uint32_t slot = 0;
+            bool found = true;
+            if (valid) {
+                const Sub m = child(s, k, select_bit(qb, j), d, pl);
+                leaf = apply(s, m, pl);
+                enc = pe | ((uint64_t)m.enc << shift);
+                found = probe_lane<LOG_SLOTS>(tab, (uint32_t)leaf.lo, (uint32_t)(leaf.lo >> 32), leaf.hi, leaf.k3, slot);
+            }
+            commit<true>(__ballot(valid && !found), leaf, enc, slot, len);
+            if (ovf) return;
+        }
     }
 
     // handle_non_doubles (handle_moves.py:109-200); the pre-scan (:144-155) is
@@ -457,13 +494,7 @@ struct Gen {
             batch(a1, t1, (uint64_t)e1, 1);
             return;
         }
-        for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
-            const int i = __builtin_ctz(b1);
-            const Kids k2{rdl(q2, i), (int)rdl((uint32_t)x2, i)};
-            if (!k2.bits) continue;
-            leaf_batch(rd_node(t1, i), k2, db, (uint64_t)rdl(e1, i), 16, 2);
-            if (ovf) return;
-        }
+        flat_leaves(__ballot(a1 && q2 != 0u), t1, q2, x2, (uint64_t)e1, db, 16, 2);
     }
 
     // Revisit check of a sibling batch at one depth: returns the lanes not seen
@@ -552,27 +583,21 @@ struct Gen {
                 BG_T1(15, tx);
                 for (uint64_t b3 = f3; b3; b3 &= b3 - 1ull) {
                     const int i3 = __ffsll((unsigned long long)b3) - 1;
-                    const Kids k4{rdl(q4, i3), (int)rdl((uint32_t)x4, i3)};
-                    const uint64_t m3 = m2 | ((uint64_t)rdl(e3l, i3) << 32);
-                    if (!k4.bits) {
-                        if (!got4) { insert(rd_node(t3, i3), m3, 3); if (ovf) return; }
+                    const uint32_t kb = rdl(q4, i3);
+                    if (!kb) {
+                        if (!got4) {
+                            insert(rd_node(t3, i3), m2 | ((uint64_t)rdl(e3l, i3) << 32), 3);
+                            if (ovf) return;
+                        }
                         continue;
                     }
-                    // got4 holds from this node's leaves on, so dead ends up to the
-                    // next node with children are no-ops: pair the two nodes' leaves
-                    const uint64_t withkids = __ballot(((f3 >> (threadIdx.x & 63)) & 1ull) && q4 != 0u);
-                    const uint64_t later = withkids & (b3 & (b3 - 1ull));
-                    if (later) {
-                        const int j3 = __ffsll((unsigned long long)later) - 1;
-                        const Kids kB{rdl(q4, j3), (int)rdl((uint32_t)x4, j3)};
-                        const uint64_t mB = m2 | ((uint64_t)rdl(e3l, j3) << 32);
-                        pair_batch(rd_node(t3, i3), k4, m3, rd_node(t3, j3), kB, mB, d, 48, 4);
-                        b3 &= ~((2ull << j3) - 1ull) | (1ull << i3);   // drop everything up to j3 (i3 by the loop)
-                    } else {
-                        leaf_batch(rd_node(t3, i3), k4, d, m3, 48, 4);
-                    }
+                    // from the first node with children on, got4 holds: dead ends are
+                    // no-ops and every remaining node's leaves go out as one flat batch
+                    const uint64_t rest = b3 & __ballot(q4 != 0u);
+                    flat_leaves(rest, t3, q4, x4, m2 | ((uint64_t)e3l << 32), d, 48, 4);
                     if (ovf) return;
                     got4 = true;
+                    break;
                 }
             }
         }

@@ -130,7 +130,7 @@ struct MinSink {
         if (slot == kKeyCap - 1) flush(kKeyCap);
     }
 
-    // keys of the lanes in m (<= 32 of them), list positions idx0, idx0+1, ...
+    // keys of the lanes in m (<= 64 of them < kKeyCap), list positions idx0, idx0+1, ...
     __device__ __forceinline__ void push_lanes(uint64_t m, const Node& t, uint64_t, int idx0) {
         const int pos = idx0 % kKeyCap, n = __popcll(m);
         const int r = lane_rank(m);
