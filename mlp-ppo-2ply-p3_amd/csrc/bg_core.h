@@ -499,7 +499,9 @@ struct Gen {
 
     // Revisit check of a sibling batch at one depth: returns the lanes not seen
     // before and records them (while the memo has room).
-    template <int LOGM>
+    // DEDUP: the batch may hold equal states (cousins); the first in lane order is
+    // the visit, later ones are revisits (pruned) -- when recorded.
+    template <int LOGM, bool DEDUP = false>
     __device__ __forceinline__ uint64_t memo_batch(uint4* memo, int& nm, bool act, const Node& t, uint32_t tag) {
         if (!memo) return __ballot(act);
         constexpr int LOGT = MEMO_KIND == 1 ? kLogCMemo : LOGM;
@@ -518,12 +520,63 @@ struct Gen {
         else if (MEMO_KIND == 1) room = ((7 << kLogCMemo) / 8) - n_memo2 - n_memo3;
         else room = min(((7 << LOGM) / 8) - nm, cap_unique / 3 - n_memo2 - n_memo3);
         while (n > room && rec) { rec &= ~(1ull << (63 - __clzll((long long)rec))); --n; }
+        uint64_t kept = rec;
         if (rec) {
-            if (TAGGED) place_batch<LOG_SLOTS, false>(tab, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
-            else place_batch<LOGT, false>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            if (TAGGED) kept = place_batch<LOG_SLOTS, DEDUP>(tab, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
+            else kept = place_batch<LOGT, DEDUP>(memo, rec, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, k3, slot);
         }
-        nm += n;
-        return fresh;
+        nm += __popcll(kept);
+        return fresh & ~(rec & ~kept);
+    }
+
+    // Once got4 holds (dead ends are no-ops), the rest of a depth-1 subtree runs
+    // level by level in DFS order: all depth-3 children of the depth-2 nodes on
+    // the lanes in `parents` (lane order = DFS order), 64 at a time, the revisit
+    // check (first in lane order wins) and each chunk's leaves as one flat batch.
+    __device__ __forceinline__ void flat_depth3(uint64_t parents, const Node& t2, uint32_t q3, int x3, uint64_t penc2,
+                                                int d) {
+        const int l = threadIdx.x & 63;
+        const bool par = (parents >> l) & 1ull;
+        const uint32_t cnt = par ? (uint32_t)__popc(q3) : 0u;
+        uint32_t pre = 0, total = 0;
+        const uint64_t below = (1ull << l) - 1ull;
+        #pragma unroll
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t m = __ballot((cnt >> b) & 1u);
+            pre += (uint32_t)__popcll(m & below) << b;
+            total += (uint32_t)__popcll(m) << b;
+        }
+        const uint64_t live = __ballot(cnt != 0u);
+        for (uint32_t c = 0; c < total; c += 64) {
+            const uint32_t pp = c + (uint32_t)l;
+            const bool valid = pp < total;
+            int src = 0;
+            for (uint64_t m = live; m; m &= m - 1ull) {
+                const int i = __ffsll((unsigned long long)m) - 1;
+                const uint32_t pi = rdl(pre, i);
+                if (pi >= c + 64u) break;
+                src = pp >= pi ? i : src;
+            }
+            const uint32_t qb = (uint32_t)__shfl((int)q3, src);
+            const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
+            const Node s2 = shfl_node(t2, src);
+            const Kids k{qb, __shfl(x3, src)};
+            const uint64_t pe = (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc2, src) |
+                                ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(penc2 >> 32), src) << 32);
+            Node t3;
+            uint64_t pe3 = 0;
+            if (valid) {
+                const Sub m = child(s2, k, select_bit(qb, j), d, pl);
+                t3 = apply(s2, m, pl);
+                pe3 = pe | ((uint64_t)m.enc << 32);
+            }
+            const uint64_t f3 = memo_batch<kLogMemo3, true>(memo3, n_memo3, valid, t3, kTag3);
+            uint32_t q4 = 0;
+            int x4 = -1;
+            if ((f3 >> l) & 1ull) { const Kids kk = gen(t3, d, pl, blocked); q4 = kk.bits; x4 = kk.extra; }
+            flat_leaves(__ballot(((f3 >> l) & 1ull) && q4 != 0u), t3, q4, x4, pe3, d, 48, 4);
+            if (ovf) return;
+        }
     }
 
     // handle_doubles (handle_moves.py:203-310): 4-deep pre-order DFS; partial
@@ -563,6 +616,11 @@ struct Gen {
             int x3 = -1;
             if ((f2 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; x3 = k.extra; }
             for (uint64_t b2 = f2; b2; b2 &= b2 - 1ull) {
+                if (got4) {
+                    flat_depth3(b2 & __ballot(q3 != 0u), t2, q3, x3, m1 | ((uint64_t)e2l << 16), d);
+                    if (ovf) return;
+                    break;
+                }
                 const int i2 = __ffsll((unsigned long long)b2) - 1;
                 const Node s2 = rd_node(t2, i2);
                 const Kids k3{rdl(q3, i2), (int)rdl((uint32_t)x3, i2)};
