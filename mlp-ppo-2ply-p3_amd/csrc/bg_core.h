@@ -579,6 +579,53 @@ struct Gen {
         }
     }
 
+    // The same one level up: the depth-2 children of the depth-1 nodes on the
+    // lanes in `parents`, 64 at a time, revisit check, then flat_depth3 per chunk.
+    __device__ __forceinline__ void flat_depth2(uint64_t parents, const Node& t1, uint32_t q2, int x2, uint64_t penc1,
+                                                int d) {
+        const int l = threadIdx.x & 63;
+        const bool par = (parents >> l) & 1ull;
+        const uint32_t cnt = par ? (uint32_t)__popc(q2) : 0u;
+        uint32_t pre = 0, total = 0;
+        const uint64_t below = (1ull << l) - 1ull;
+        #pragma unroll
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t m = __ballot((cnt >> b) & 1u);
+            pre += (uint32_t)__popcll(m & below) << b;
+            total += (uint32_t)__popcll(m) << b;
+        }
+        const uint64_t live = __ballot(cnt != 0u);
+        for (uint32_t c = 0; c < total; c += 64) {
+            const uint32_t pp = c + (uint32_t)l;
+            const bool valid = pp < total;
+            int src = 0;
+            for (uint64_t m = live; m; m &= m - 1ull) {
+                const int i = __ffsll((unsigned long long)m) - 1;
+                const uint32_t pi = rdl(pre, i);
+                if (pi >= c + 64u) break;
+                src = pp >= pi ? i : src;
+            }
+            const uint32_t qb = (uint32_t)__shfl((int)q2, src);
+            const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
+            const Node s1 = shfl_node(t1, src);
+            const Kids k{qb, __shfl(x2, src)};
+            const uint64_t pe = (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc1, src);
+            Node t2;
+            uint64_t pe2 = 0;
+            if (valid) {
+                const Sub m = child(s1, k, select_bit(qb, j), d, pl);
+                t2 = apply(s1, m, pl);
+                pe2 = pe | ((uint64_t)m.enc << 16);
+            }
+            const uint64_t f2 = memo_batch<kLogMemo2, true>(memo2, n_memo2, valid, t2, kTag2);
+            uint32_t q3 = 0;
+            int x3 = -1;
+            if ((f2 >> l) & 1ull) { const Kids kk = gen(t2, d, pl, blocked); q3 = kk.bits; x3 = kk.extra; }
+            flat_depth3(__ballot(((f2 >> l) & 1ull) && q3 != 0u), t2, q3, x3, pe2, d);
+            if (ovf) return;
+        }
+    }
+
     // handle_doubles (handle_moves.py:203-310): 4-deep pre-order DFS; partial
     // prefixes are inserted at dead ends only until the first 4-long sequence.
     // Each node's children are expanded one per lane (state, revisit check,
@@ -599,6 +646,10 @@ struct Gen {
         int x2 = -1;
         if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; x2 = k.extra; }
         for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
+            if (got4) {
+                flat_depth2((uint64_t)b1 & __ballot(q2 != 0u), t1, q2, x2, (uint64_t)e1, d);
+                return;
+            }
             const int i1 = __builtin_ctz(b1);
             const Node s1 = rd_node(t1, i1);
             const Kids k2{rdl(q2, i1), (int)rdl((uint32_t)x2, i1)};
