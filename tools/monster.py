@@ -35,7 +35,7 @@ for i in order:
         names = ["dbl", "", "d2 batches", "d2 fresh", "d3 batches", "d3 fresh", "leaf batches", "leaf probes",
                  "committed", "", "", "d2 kids", "d3 kids"]
         print("   ", ", ".join("%s %.0f" % (names[k], v[k]) for k in (2, 3, 11, 4, 5, 12, 6, 7, 8)))
-        print("    cycles(memtime): doubles %.0f  leaf batches %.0f (commit %.0f)  d3 expand %.0f" % (v[1], v[14], v[13], v[15]))
+        print("    cycles(memtime): doubles %.0f  flat leaves %.0f (commit %.0f)  memo checks %.0f" % (v[1], v[14], v[13], v[15]))
 for r in res:
     print("pos %2d dice %d-%d n_total %4d  movegen %7.1f us  (in-step wave %.1f us)" % (r[0], r[1], r[1], r[2], r[3], r[4]))
 print("mean us", np.mean([r[3] for r in res]))
