@@ -338,11 +338,11 @@ struct MoveSink {
     uint64_t* out;      // this game's move list, `cap` entries
     int cap;
     __device__ __forceinline__ void reset() {}
-    __device__ __forceinline__ void push(const Node&, uint64_t enc, int idx) {
+    __device__ __forceinline__ void push(const Node&, uint64_t enc, int idx, int /*len*/) {
         if (idx < cap && (threadIdx.x & 63) == 0) out[idx] = enc;
     }
     // entries of the lanes in m (lane order) at idx0, idx0+1, ...
-    __device__ __forceinline__ void push_lanes(uint64_t m, const Node&, uint64_t enc, int idx0) {
+    __device__ __forceinline__ void push_lanes(uint64_t m, const Node&, uint64_t enc, int idx0, int /*len*/) {
         const int idx = idx0 + lane_rank(m);
         if (((m >> (threadIdx.x & 63)) & 1ull) && idx < cap) out[idx] = enc;
     }
@@ -378,7 +378,7 @@ struct Gen {
         if (fill() >= cap_unique) { ovf = true; return; }
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
-            sink.push(s, enc, count);
+            sink.push(s, enc, count, len);
             ++count;
         }
     }
@@ -410,7 +410,7 @@ struct Gen {
         n_unique += n;
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
-            sink.push_lanes(fresh, t, enc, count);
+            sink.push_lanes(fresh, t, enc, count, len);
             count += n;
         }
         BG_T1(13, tc);
@@ -719,6 +719,12 @@ struct Gen {
         pass_nd(s0, hi, lo);
         if (ovf) return;
         if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi);   // :41-53
+    }
+
+    // doubles only (r0 == r1 == d)
+    __device__ __forceinline__ void run_d(const Node& s0, int d) {
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
+        doubles(s0, d);
     }
 
     // get_all_possible_moves (get_all_moves.py:9-70)

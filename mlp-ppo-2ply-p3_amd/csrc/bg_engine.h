@@ -403,4 +403,6 @@ struct bgx_engine {
     // bg_search.hip workspace (grown on demand)
     void* search_ws;
     size_t search_ws_bytes;
+    void* search_pool;        // 2-ply leaf pool: keys [cap] x 16 B, then tags [cap] x 4 B
+    size_t search_pool_cap;
 };

@@ -499,7 +499,7 @@ int bgx_engine_destroy(bgx_engine* e) {
     (void)hipSetDevice(e->device);
     Args& A = e->a;
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
-                    e->slow_tables, e->search_ws, A.stamps, e->perm, A.cls, e->order_cnt};
+                    e->slow_tables, e->search_ws, e->search_pool, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete e;
     return BGX_OK;

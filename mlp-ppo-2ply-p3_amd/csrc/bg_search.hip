@@ -4,13 +4,26 @@
 // 2-ply, per root lane (board, mover, roll) with legal afterstates a_0..a_{n-1}:
 //   Q(a) = sum_r p_r * min_{b in replies(a, r)} V(enc(b, opponent))       (leaf = a if no reply)
 //   best = first argmax_a Q(a)
-// Work item ("job") = (afterstate row, roll r): one wave enumerates the
-// opponent's replies with the exact reference move generator (bg_core.h, LDS
-// dedup + revisit memo), keeps the surviving afterstate KEYS in an LDS list,
-// and evaluates them 32 at a time: features are generated on the fly from
-// (afterstate bytes, key) and fed as the B operand of v_mfma_f32_32x32x2_f32
-// (W1 . F^T), the value is a dot with the value head in registers, and the wave
-// keeps the running minimum.  Leaves never touch HBM.
+// Work item ("job") = (afterstate row, roll r).  The pipeline is decoupled:
+//   k_rows    one wave per row: the afterstate a as a 64-byte record + the
+//             mover's side of a (16 B) for the evaluator;
+//   k_enum    one wave per job (persistent, grid-stride): the opponent's replies
+//             with the exact reference move generator (bg_core.h, LDS dedup +
+//             revisit memo), each surviving-candidate afterstate KEY (16 B) and a
+//             tag (job, sub-move count) streamed to an HBM leaf pool in 256-slot
+//             blocks; three variants: non-doubles rolls (4 KiB of LDS, no doubles
+//             code), doubles rolls (dedup table + memo), and an explicit job list;
+//   k_enum_slow  jobs whose dedup set outgrew LDS, on 2 MiB HBM tables;
+//   k_eval    dense pass over the pool: features from (row side, key) as exact
+//             f16 values, W1 split hi+lo on v_mfma_f32_32x32x16_f16, value head
+//             in registers, segmented min per job + atomicMin into minv[job];
+//   k_two_ply_reduce  Q(a) and the first argmax.
+// The reference's filter_full_moves_by_max_submoves (get_all_moves.py:73-94) is
+// applied by the evaluator: a leaf counts iff its sub-move count equals the
+// job's final maximum (written at job end), which is exactly "first insertion
+// of an afterstate had the maximal length" -- the surviving set.  A job whose
+// pool allocation failed is re-run in a later round (a min over a subset of
+// leaves plus the min over all of them is the min over all of them).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -22,10 +35,14 @@ using namespace bg;
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int kK1 = 99;            // 198 / 2 k-steps of 32x32x2
-constexpr int kKeyCap = 512;       // LDS reply-key list per wave (8 KiB), flushed when full
-constexpr int kSearchLog = 10;     // LDS dedup table (16 KiB)
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kK1 = 99;            // 198 / 2 k-steps of 32x32x2 (f32 section, 1-ply)
+constexpr int kKB = 13;            // 208 / 16 k-steps of 32x32x16 (f16 section, 2-ply)
 constexpr int kSlowQueue = 1 << 20;
+constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
+constexpr uint32_t kTagNone = 0xFFFFFFFFu;
+constexpr int kLogLight = 8;       // non-doubles reply enumeration: 256-slot table (4 KiB)
+constexpr int kMaxRounds = 256;
 
 __constant__ float kOff15s[16] = {
     0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
@@ -34,13 +51,37 @@ __constant__ float kOff15s[16] = {
 // get_all_dice_rolls_tensor (get_all_dice_rolls.py:5-34): (1,1),(1,2),...,(6,6)
 __constant__ uint8_t kRoll0[21] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6};
 __constant__ uint8_t kRoll1[21] = {1, 2, 3, 4, 5, 6, 2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6, 6};
+// roll indices of the 15 non-doubles and the 6 doubles
+__constant__ uint8_t kNdRoll[15] = {1, 2, 3, 4, 5, 7, 8, 9, 10, 12, 13, 14, 16, 17, 19};
+__constant__ uint8_t kDbRoll[6] = {0, 6, 11, 15, 18, 20};
 
 __device__ __forceinline__ int hid(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// Value net packed for MFMA (bgx_value_pack): w1p [99][T][64], b1p [T][16][64],
-// wvp [T][16][64] (= value_head.weight[32t + hid(r, l>>5)]), then bv.
+// Value net packed for MFMA (bgx_value_pack), in floats:
+//   f32 section (1-ply):  w1p [99][T][64], b1p [T][16][64], wvp [T][16][64]
+//                         (= value_head.weight[32t + hid(r, l>>5)]), bv, 3 pad
+//   f16 section (2-ply):  hdr [4] (e1 as int bits), w1q [13][T][2][64] x uint4:
+//                         lane l, part 0 = hi / 1 = lo of W1s[32t + (l&31)][kperm(kb, l>>5, i)],
+//                         i = 0..7, W1s = W1 * 2^e1 with the two `off` columns divided by 15
+//                         (the features are then exact small integers / halves in f16).
 struct VNet { const float* w1p; const float* b1p; const float* wvp; float bv; };
 
+__host__ __device__ inline int sz_f32(int T) { return kK1 * T * 64 + 2 * T * 16 * 64 + 4; }
+__host__ __device__ inline int sz_f16(int T) { return 4 + kKB * T * 2 * 64 * 4; }
+
+// Permuted K order of the f16 section: k-blocks 0-5 = P1 points, 6-11 = P2 points
+// (lane half h of block kb holds points 2pp, 2pp+1 with pp = 2(kb%6) + h, four
+// units each), block 12 = [bar1, off1, bar2, off2, onehot0, onehot1] on h = 0.
+// Returns the reference feature index (immutable_board.py:171-212) or -1 (pad).
+__host__ __device__ inline int kperm(int kb, int h, int i) {
+    if (kb < 12) {
+        const int P = kb / 6, pp = 2 * (kb % 6) + h, point = 2 * pp + (i >> 2);
+        return 98 * P + 4 * point + (i & 3);
+    }
+    if (h) return -1;
+    const int ex[8] = {96, 97, 194, 195, 196, 197, -1, -1};
+    return ex[i];
+}
 // Feature k of the board (root bytes `ab` in LDS) after player q moved to the
 // afterstate with key (klo, khi, k3): q's counts come from the key nibbles, the
 // other side's from ab minus the hit blots; one-hot = `cur`.
@@ -101,51 +142,6 @@ __device__ __forceinline__ float wave_min(float v) {
     return v;
 }
 
-// Sink for the reply enumeration: afterstate keys -> LDS list -> batched V -> min.
-template <int T>
-struct MinSink {
-    uint4* klist;
-    const uint8_t* ab;
-    VNet vn;
-    int q;
-    float best;
-    int evaluated;
-
-    __device__ __forceinline__ void reset() { best = INFINITY; }
-
-    __device__ __attribute__((noinline)) void flush(int n) {
-        const int l = threadIdx.x & 63, j = l & 31;
-        for (int base = 0; base < n; base += 32) {
-            const uint4 k = klist[base + (j < n - base ? j : 0)];
-            const float v = eval_rows<T>(vn, ab, (uint64_t)k.x | ((uint64_t)k.y << 32), k.z, k.w, q, q);
-            best = fminf(best, wave_min(j < n - base ? v : INFINITY));
-        }
-        evaluated += n;
-    }
-
-    __device__ __forceinline__ void push(const Node& s, uint64_t, int idx) {
-        const int slot = idx % kKeyCap;
-        if ((threadIdx.x & 63) == 0) klist[slot] = make_uint4((uint32_t)s.lo, (uint32_t)(s.lo >> 32), s.hi, s.k3);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (slot == kKeyCap - 1) flush(kKeyCap);
-    }
-
-    // keys of the lanes in m (<= 64 of them < kKeyCap), list positions idx0, idx0+1, ...
-    __device__ __forceinline__ void push_lanes(uint64_t m, const Node& t, uint64_t, int idx0) {
-        const int pos = idx0 % kKeyCap, n = __popcll(m);
-        const int r = lane_rank(m);
-        const bool on = (m >> (threadIdx.x & 63)) & 1ull;
-        const uint4 key = make_uint4((uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3);
-        if (on && pos + r < kKeyCap) klist[pos + r] = key;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        if (pos + n >= kKeyCap) {
-            flush(kKeyCap);
-            if (on && pos + r >= kKeyCap) klist[pos + r - kKeyCap] = key;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        }
-    }
-};
-
 __device__ __forceinline__ uint64_t uload64(const uint64_t* p) {
     const uint64_t v = *p;
     // cast through uint32_t: the builtin returns int, and sign extension would
@@ -164,96 +160,420 @@ __device__ __forceinline__ Node apply_move(Node s, uint64_t m, int pl) {
     return s;
 }
 
-struct SearchArgs {
-    const int32_t* row_lane;     // [rows] root lane of each afterstate row
-    const int32_t* lane_off;     // [B] first row of each lane
-    const int64_t* rows_total;   // device scalar
-    float* minv;                 // [rows][21]
-    unsigned long long* leaves;  // device counter
-    int32_t* slow_count;         // overflow queue
-    int32_t* slow_queue;
+// ------------------------------------------------------------------ 2-ply --
+struct S2 {
+    const uint8_t* rowrec;            // [rows][64]: afterstate bytes 0..51, byte 52 = replier q
+    int32_t rows;
+    uint4* keys;                      // leaf pool [cap]
+    uint32_t* tags;                   // [cap] job | len << 29, kTagNone = unused slot
+    unsigned long long* cursor;       // next free pool slot (kBlk granularity; may run past cap)
+    unsigned long long cap;
+    uint8_t* maxlen;                  // [jobs] final max sub-move count (0xFF = not finished)
+    unsigned long long* leaves;       // surviving-leaf counter (stats)
+    int32_t* slow_count;
+    int32_t* slow_queue;              // [kSlowQueue]
+    int32_t* retry_count;
+    int32_t* retry_list;              // [jobs]
+    const int32_t* list;              // explicit job list (variant 2)
+    const int32_t* list_count;
+    int32_t* err;
+    int cap_light, cap_heavy;         // unique-entry capacity of the LDS tables (tests shrink them)
 };
 
-// One (row, roll) job: opponent reply enumeration + leaf minimum.
-template <int LOG, typename SlotPtr, int T>
-__device__ __forceinline__ bool two_ply_job(const Args& A, const SearchArgs& S, const VNet& vn, int64_t job,
-                                            SlotPtr tab, int cap_unique, uint4* memo, uint4* klist, uint8_t* ab) {
-    const int64_t row = job / 21;
-    const int r = (int)(job - row * 21);
-    const int lane_g = S.row_lane[row];
-    const int a = (int)(row - S.lane_off[lane_g]);
-    const int l = threadIdx.x & 63;
-    int bv = load_rec(A, lane_g);
-    const int mover = rd(bv, R_CUR);
-    const uint64_t m = uload64(A.moves + (size_t)lane_g * A.max_moves + a);
-    uint32_t blocked;
-    Node s = node_from_bytes(bv, mover, blocked);
-    s = apply_move(s, m, mover);
-    const int bva = bytes_from_node(bv, s, mover);      // the afterstate a, one byte per lane
-    if (l < 64) ab[l] = (uint8_t)bva;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const int q = 1 - mover;
-    // clear tables
-    for (int i = l; i < (1 << LOG); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
-    const int r0 = kRoll0[r], r1 = kRoll1[r];
-    if (r0 == r1)
-        for (int i = l; i < kMemoSlots; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    Gen<LOG, SlotPtr, MinSink<T>> g;
-    g.tab = tab; g.pl = q; g.cap_unique = cap_unique;
-    g.memo2 = r0 == r1 ? memo : nullptr;
-    g.memo3 = r0 == r1 ? memo + (1 << kLogMemo2) : nullptr;
-    g.sink.klist = klist; g.sink.ab = ab; g.sink.vn = vn; g.sink.q = q; g.sink.best = INFINITY;
-    g.sink.evaluated = 0;
-    uint32_t blk;
-    const Node sq = node_from_bytes(bva, q, blk);
-    g.blocked = blk;
-    g.run(sq, r0, r1);
-    if (g.ovf) return false;
-    const int rem = g.count % kKeyCap;
-    if (g.count == 0) {                 // no reply: the opponent passes, the leaf is a itself
-        if (l == 0) klist[0] = make_uint4((uint32_t)sq.lo, (uint32_t)(sq.lo >> 32), sq.hi, sq.k3);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        g.sink.flush(1);
-    } else if (rem) {
-        g.sink.flush(rem);
-    }
-    if (l == 0) {
-        S.minv[row * 21 + r] = g.sink.best;
-        atomicAdd(S.leaves, (unsigned long long)(g.count ? g.count : 1));
-    }
-    return true;
+__device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
+    return (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
 }
 
-template <int T>
-__global__ __launch_bounds__(64) void k_two_ply(Args A, SearchArgs S, VNet vn) {
-    __shared__ uint4 tab[1 << kSearchLog];
+// Gen sink of the reply enumeration: every entry of the current maximal length
+// goes to the leaf pool as (key, job | len << 29); the wave owns a kBlk-slot
+// block at a time (one atomic per block).  On pool exhaustion the job is `lost`
+// (re-run next round); its leaves already written stay valid candidates.
+struct KeySink {
+    uint4* keys;
+    uint32_t* tags;
+    unsigned long long* cursor;
+    unsigned long long cap;
+    unsigned long long blk;
+    int fill;
+    uint32_t job;
+    bool lost;
+
+    __device__ __forceinline__ void reset() {}
+
+    __device__ __forceinline__ void push_lanes(uint64_t m, const Node& t, uint64_t, int, int len) {
+        if (lost) return;
+        const int n = __popcll(m);
+        const int l = threadIdx.x & 63;
+        const bool on = (m >> l) & 1ull;
+        int p = fill + lane_rank(m);
+        unsigned long long b = blk;
+        if (fill + n > kBlk) {
+            unsigned long long nb = 0;
+            if (l == 0) nb = atomicAdd(cursor, (unsigned long long)kBlk);
+            nb = bcast64(nb);
+            if (nb + kBlk > cap) { lost = true; return; }
+            if (p >= kBlk) { b = nb; p -= kBlk; }
+            blk = nb;
+            fill = fill + n - kBlk;
+        } else {
+            fill += n;
+        }
+        if (on) {
+            keys[b + p] = make_uint4((uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3);
+            tags[b + p] = job | ((uint32_t)len << 29);
+        }
+    }
+    __device__ __forceinline__ void push(const Node& s, uint64_t enc, int idx, int len) {
+        push_lanes(1ull, s, enc, idx, len);
+    }
+    // mark the unused tail of the wave's current block
+    __device__ __forceinline__ void finish() {
+        for (int i = fill + (threadIdx.x & 63); i < kBlk; i += 64) tags[blk + i] = kTagNone;
+    }
+};
+
+// One (row, roll) job.  KIND 0: non-doubles roll, 1: doubles roll, 2: either.
+// Returns 0 done, 1 LDS/HBM table overflow, 2 pool exhausted.
+template <int LOG, typename SlotPtr, bool MEMO, int KIND>
+__device__ __forceinline__ int enum_job(const S2& S, int job, SlotPtr tab, int cap_unique, uint4* memo,
+                                        KeySink& sink, unsigned long long& leaves) {
+    const int row = job / 21, r = job - row * 21;
+    const int r0 = kRoll0[r], r1 = kRoll1[r];
+    const int l = lane_id();
+    const int bv = (int)S.rowrec[(size_t)row * 64 + l];
+    const int q = rd(bv, 52);
+    uint32_t blocked;
+    const Node sq = node_from_bytes(bv, q, blocked);
+    for (int i = l; i < (1 << LOG); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
+    const bool dbl = KIND == 1 || (KIND == 2 && r0 == r1);
+    if (MEMO && dbl)
+        for (int i = l; i < kMemoSlots; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    Gen<LOG, SlotPtr, KeySink> g;
+    g.tab = tab; g.pl = q; g.cap_unique = cap_unique; g.blocked = blocked;
+    g.memo2 = MEMO && dbl ? memo : nullptr;
+    g.memo3 = MEMO && dbl ? memo + (1 << kLogMemo2) : nullptr;
+    g.sink = sink;
+    g.sink.job = (uint32_t)job;
+    g.sink.lost = false;
+    if (KIND == 0) g.run_nd(sq, r0, r1);
+    else if (KIND == 1) g.run_d(sq, r0);
+    else g.run(sq, r0, r1);
+    if (!g.ovf && g.count == 0) g.sink.push(sq, 0ull, 0, 0);     // no reply: the leaf is a itself
+    sink = g.sink;
+    if (g.ovf) return 1;
+    if (sink.lost) return 2;
+    if (l == 0) S.maxlen[job] = (uint8_t)g.cur_max;
+    leaves += (unsigned long long)(g.count ? g.count : 1);
+    return 0;
+}
+
+__device__ __forceinline__ void queue_job(int32_t* count, int32_t* list, int cap, int job, int32_t* overflow_count,
+                                          int32_t* overflow_list) {
+    if (lane_id() != 0) return;
+    const int i = atomicAdd(count, 1);
+    if (i < cap) { list[i] = job; return; }
+    atomicSub(count, 1);
+    overflow_list[atomicAdd(overflow_count, 1)] = job;
+}
+
+__device__ __forceinline__ KeySink make_sink(const S2& S) {
+    KeySink k;
+    k.keys = S.keys; k.tags = S.tags; k.cursor = S.cursor; k.cap = S.cap;
+    k.blk = 0; k.fill = kBlk; k.job = 0; k.lost = false;
+    return k;
+}
+
+// VARIANT 0: jobs (row, non-doubles roll) implicit, 1: (row, doubles roll)
+// implicit, 2: the explicit list.
+template <int LOG, bool MEMO, int VARIANT>
+__global__ __launch_bounds__(64) void k_enum(S2 S) {
+    __shared__ uint4 tab[1 << LOG];
+    __shared__ uint4 memo_[MEMO ? kMemoSlots : 1];
+    uint4* memo = MEMO ? memo_ : nullptr;
+    KeySink sink = make_sink(S);
+    unsigned long long leaves = 0;
+    const int64_t n = VARIANT == 0 ? (int64_t)S.rows * 15 : VARIANT == 1 ? (int64_t)S.rows * 6 : *S.list_count;
+    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
+        int job;
+        if (VARIANT == 0) { const int row = (int)(i / 15); job = row * 21 + kNdRoll[i - (int64_t)row * 15]; }
+        else if (VARIANT == 1) { const int row = (int)(i / 6); job = row * 21 + kDbRoll[i - (int64_t)row * 6]; }
+        else job = S.list[i];
+        const int st = enum_job<LOG, uint4*, MEMO, VARIANT>(S, job, tab, VARIANT == 0 ? S.cap_light : S.cap_heavy, memo,
+                                                             sink, leaves);
+        if (st == 1) queue_job(S.slow_count, S.slow_queue, kSlowQueue, job, S.retry_count, S.retry_list);
+        else if (st == 2) queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
+    }
+    sink.finish();
+    if (lane_id() == 0 && leaves) atomicAdd(S.leaves, leaves);
+}
+
+// Jobs whose dedup set outgrew the LDS table: 131,072-slot HBM table per wave.
+__global__ __launch_bounds__(64) void k_enum_slow(S2 S, uint4* tables) {
     __shared__ uint4 memo[kMemoSlots];
-    __shared__ uint4 klist[kKeyCap];
-    __shared__ uint8_t ab[64];
-    const int64_t njobs = (int64_t)(*S.rows_total) * 21;
-    for (int64_t job = blockIdx.x; job < njobs; job += gridDim.x) {
-        if (!two_ply_job<kSearchLog, uint4*, T>(A, S, vn, job, tab, cap_fast<kSearchLog>(), memo, klist, ab)) {
-            if ((threadIdx.x & 63) == 0) {
-                const int qi = atomicAdd(S.slow_count, 1);
-                if (qi < kSlowQueue) S.slow_queue[qi] = (int32_t)job;
-                else atomicOr(A.err, 2);
+    uint4* tab = tables + ((size_t)blockIdx.x << kLogSlotsSlow);
+    KeySink sink = make_sink(S);
+    unsigned long long leaves = 0;
+    const int n = min(*S.slow_count, kSlowQueue);
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int job = S.slow_queue[i];
+        const int st = enum_job<kLogSlotsSlow, uint4*, true, 2>(S, job, tab, kCapSlow, memo, sink, leaves);
+        if (st == 1 && lane_id() == 0) atomicOr(S.err, 1);
+        else if (st == 2) queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
+    }
+    sink.finish();
+    if (lane_id() == 0 && leaves) atomicAdd(S.leaves, leaves);
+}
+
+// The afterstate of every row (root lane, legal move a): 64-byte record for the
+// enumerators and the mover's side of a (nibbles, bar, off, replier q) for k_eval.
+__global__ __launch_bounds__(256) void k_rows(Args A, const int32_t* row_lane, const int32_t* lane_off, int32_t rows,
+                                              uint8_t* rowrec, uint4* rowside) {
+    const int l = lane_id();
+    const int nw = gridDim.x * (blockDim.x >> 6);
+    for (int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < rows; row += nw) {
+        const int lane_g = row_lane[row];
+        const int a = row - lane_off[lane_g];
+        const int bv = load_rec(A, lane_g);
+        const int mover = rd(bv, R_CUR);
+        const uint64_t m = uload64(A.moves + (size_t)lane_g * A.max_moves + a);
+        uint32_t blocked;
+        Node s = node_from_bytes(bv, mover, blocked);
+        s = apply_move(s, m, mover);
+        const int bva = bytes_from_node(bv, s, mover);
+        const int q = 1 - mover;
+        rowrec[(size_t)row * 64 + l] = (uint8_t)(l < 52 ? bva : (l == 52 ? q : 0));
+        if (l == 0)
+            rowside[row] = make_uint4((uint32_t)s.lo, (uint32_t)(s.lo >> 32), s.hi,
+                                      (s.k3 & 15u) | (((s.k3 >> 4) & 15u) << 4) | ((uint32_t)q << 8));
+    }
+}
+
+// ---- leaf evaluation on f16 MFMA ----
+// bit i of x (i < 16) -> bit 4i
+__device__ __forceinline__ uint64_t spread4(uint32_t x) {
+    uint64_t v = x & 0xFFFFu;
+    v = (v | (v << 24)) & 0x000000FF000000FFull;
+    v = (v | (v << 12)) & 0x000F000F000F000Full;
+    v = (v | (v << 6)) & 0x0303030303030303ull;
+    v = (v | (v << 3)) & 0x1111111111111111ull;
+    return v;
+}
+
+struct Leaf {
+    uint64_t lo[2];    // P1, P2 point counts 0..15 (nibbles)
+    uint32_t hi[2];    // points 16..23
+    uint32_t bar[2], off[2];
+    int q, job;
+    bool valid;
+};
+
+struct EvalArgs {
+    const uint4* keys;
+    const uint32_t* tags;
+    const unsigned long long* cursor;
+    unsigned long long cap;
+    const uint4* rowside;
+    const uint8_t* maxlen;
+    int32_t* minv;                    // [jobs] ordered-int encoding of the min
+    const uint4* w1q;
+    const float* b1p;
+    const float* wvp;
+    const int* hdr;
+    float bv;
+};
+
+__device__ __forceinline__ Leaf load_leaf(const EvalArgs& E, unsigned long long i) {
+    const uint4 key = E.keys[i];
+    const uint32_t tag = E.tags[i];
+    Leaf L;
+    const bool used = tag != kTagNone;
+    const int job = used ? (int)(tag & 0x1FFFFFFFu) : 0;
+    const uint4 rs = E.rowside[job / 21];
+    L.valid = used && (uint32_t)E.maxlen[job] == (tag >> 29);
+    L.job = L.valid ? job : -1;
+    const uint32_t hits = key.w >> 8;
+    const uint64_t mlo = (((uint64_t)rs.y << 32) | rs.x) - spread4(hits & 0xFFFFu);
+    const uint32_t mhi = rs.z - (uint32_t)spread4(hits >> 16);
+    const uint32_t mbar = (rs.w & 15u) + (uint32_t)__builtin_popcount(hits), moff = (rs.w >> 4) & 15u;
+    const uint64_t qlo = ((uint64_t)key.y << 32) | key.x;
+    const uint32_t qhi = key.z, qbar = key.w & 15u, qoff = (key.w >> 4) & 15u;
+    L.q = (int)((rs.w >> 8) & 1u);
+    const bool q0 = L.q == 0;
+    L.lo[0] = q0 ? qlo : mlo;  L.lo[1] = q0 ? mlo : qlo;
+    L.hi[0] = q0 ? qhi : mhi;  L.hi[1] = q0 ? mhi : qhi;
+    L.bar[0] = q0 ? qbar : mbar;  L.bar[1] = q0 ? mbar : qbar;
+    L.off[0] = q0 ? qoff : moff;  L.off[1] = q0 ? moff : qoff;
+    return L;
+}
+
+__device__ __forceinline__ uint32_t h16(float x) {
+    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x);
+}
+
+// the four units of a point with n checkers (immutable_board.py:180-195) as f16 pairs
+__device__ __forceinline__ uint2 units16(uint32_t n) {
+    const uint32_t a = (n >= 1u ? 0x3C00u : 0u) | (n >= 2u ? 0x3C000000u : 0u);
+    const uint32_t c = n >= 3u ? (0x3C00u | (h16((float)((int)n - 3) * 0.5f) << 16)) : 0u;
+    return make_uint2(a, c);
+}
+
+// B operand of k-block kb for this lane's half h (permuted K order, kperm)
+__device__ __forceinline__ f16x8 feat16(const Leaf& L, int kb, int h) {
+    uint4 v;
+    if (kb < 12) {
+        const int P = kb / 6, pp = 2 * (kb % 6) + h;
+        const uint32_t byte = kb % 6 < 4 ? (uint32_t)(L.lo[P] >> (8 * pp)) & 0xFFu
+                                         : (L.hi[P] >> (8 * (pp - 8))) & 0xFFu;
+        const uint2 u0 = units16(byte & 15u), u1 = units16(byte >> 4);
+        v = make_uint4(u0.x, u0.y, u1.x, u1.y);
+    } else if (h == 0) {
+        v = make_uint4(h16((float)L.bar[0] * 0.5f) | (h16((float)L.off[0]) << 16),
+                       h16((float)L.bar[1] * 0.5f) | (h16((float)L.off[1]) << 16),
+                       L.q == 0 ? 0x3C00u : 0x3C000000u, 0u);
+    } else {
+        v = make_uint4(0u, 0u, 0u, 0u);
+    }
+    return __builtin_bit_cast(f16x8, v);
+}
+
+__device__ __forceinline__ int ord_f32(float v) {
+    const int b = __float_as_int(v);
+    return b >= 0 ? b : b ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
+// Pool tiles of 64 leaves (two 32-column MFMA tiles sharing the weight
+// fragments): X1s = W1s . F^T + b1 2^e1 on v_mfma_f32_32x32x16_f16 (hi and lo
+// parts of W1s, features exact), V = wv . relu(X1s 2^-e1) + bv, then per job the
+// min over its leaves (leaves of a job are contiguous in the pool).
+template <int T>
+__global__ __launch_bounds__(64) void k_eval(EvalArgs E) {
+    const int l = lane_id(), h = l >> 5, c = l & 31;
+    const unsigned long long used = *E.cursor < E.cap ? *E.cursor : E.cap;
+    const unsigned long long tiles = used / 64;
+    const int e1 = E.hdr[0];
+    const float up = ldexpf(1.0f, e1), down = ldexpf(1.0f, -e1);
+    for (unsigned long long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        Leaf L[2];
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) L[n] = load_leaf(E, tile * 64 + 32 * n + c);
+        // re-read the weight fragments every tile (L1/L2 hits) instead of letting
+        // the compiler hoist all 52 of them into 208 registers (1 wave per SIMD)
+        const uint4* w1q = E.w1q;
+        __asm__ volatile("" : "+s"(w1q));
+        f32x16 x[2][T];
+        #pragma unroll
+        for (int t = 0; t < T; ++t)
+            #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float b = E.b1p[(t * 16 + r) * 64 + l] * up;
+                x[0][t][r] = b;
+                x[1][t][r] = b;
             }
+        #pragma unroll
+        for (int kb = 0; kb < kKB; ++kb) {
+            const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
+            #pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const f16x8 ah = __builtin_bit_cast(f16x8, w1q[((kb * T + t) * 2 + 0) * 64 + l]);
+                const f16x8 al = __builtin_bit_cast(f16x8, w1q[((kb * T + t) * 2 + 1) * 64 + l]);
+                x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f0, x[0][t], 0, 0, 0);
+                x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f1, x[1][t], 0, 0, 0);
+                x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, x[0][t], 0, 0, 0);
+                x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f1, x[1][t], 0, 0, 0);
+            }
+        }
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            float v = 0.0f;
+            #pragma unroll
+            for (int t = 0; t < T; ++t)
+                #pragma unroll
+                for (int r = 0; r < 16; ++r) v = fmaf(fmaxf(x[n][t][r] * down, 0.0f), E.wvp[(t * 16 + r) * 64 + l], v);
+            v += __shfl_xor(v, 32);
+            v += E.bv;
+            int jb = L[n].job;
+            v = L[n].valid ? v : INFINITY;
+            // segmented min over equal-job runs of the 32 columns (lanes 0..31 == 32..63)
+            #pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const float v2 = __shfl_down(v, o, 32);
+                const int j2 = __shfl_down(jb, o, 32);
+                if (c + o < 32 && j2 == jb) v = fminf(v, v2);
+            }
+            const int jp = __shfl_up(jb, 1, 32);
+            if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(v));
         }
     }
 }
 
-template <int T>
-__global__ __launch_bounds__(64) void k_two_ply_slow(Args A, SearchArgs S, VNet vn, uint4* tables) {
-    __shared__ uint4 memo[kMemoSlots];
-    __shared__ uint4 klist[kKeyCap];
-    __shared__ uint8_t ab[64];
-    uint4* tab = tables + ((size_t)blockIdx.x << kLogSlotsSlow);
-    const int n = min(*S.slow_count, kSlowQueue);
-    for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        const int64_t job = S.slow_queue[i];
-        if (!two_ply_job<kLogSlotsSlow, uint4*, T>(A, S, vn, job, tab, kCapSlow, memo, klist, ab))
-            if ((threadIdx.x & 63) == 0) atomicOr(A.err, 1);
+// Q(a) = sum_r p_r minv[a][r] (fp32, r in roll order), first argmax.
+__global__ void k_two_ply_reduce(Args A, const int32_t* lane_off, const int32_t* minv, int32_t* best, float* bestq,
+                                 float* qout) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.B) return;
+    const uint8_t* rr = A.lanes + (size_t)i * 64;
+    const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
+    float bq = -INFINITY;
+    int ba = 0;
+    for (int a = 0; a < n; ++a) {
+        const int32_t* mv = minv + ((size_t)lane_off[i] + a) * 21;
+        float q = 0.0f;
+        for (int r = 0; r < 21; ++r)
+            q = fmaf(kRoll0[r] == kRoll1[r] ? 1.0f / 36.0f : 2.0f / 36.0f, unord_f32(mv[r]), q);
+        if (qout) qout[(size_t)i * A.max_moves + a] = q;
+        if (q > bq) { bq = q; ba = a; }
+    }
+    best[i] = ba;
+    if (bestq) bestq[i] = n ? bq : 0.0f;
+}
+
+__device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)x;
+    lo = (_Float16)(x - (float)hi);
+}
+
+// f16 section of the value pack (one workgroup): e1 from max |W1s|, then w1q.
+__global__ __launch_bounds__(1024) void k_value_pack16(const float* W1, int H, int T, int* hdr, _Float16* w1q) {
+    __shared__ float red[1024];
+    const int tid = threadIdx.x;
+    float mx = 0.0f;
+    for (int i = tid; i < H * 198; i += 1024) {
+        const int f = i % 198;
+        const float w = (f == 97 || f == 195) ? W1[i] / 15.0f : W1[i];
+        mx = fmaxf(mx, fabsf(w));
+    }
+    red[tid] = mx;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
+        __syncthreads();
+    }
+    int e1 = 0;
+    if (red[0] > 0.0f && red[0] < INFINITY) {
+        int qe;
+        (void)frexpf(red[0], &qe);
+        e1 = 14 - qe;
+        e1 = e1 < -100 ? -100 : (e1 > 100 ? 100 : e1);
+    }
+    if (tid == 0) { hdr[0] = e1; hdr[1] = 0; hdr[2] = 0; hdr[3] = 0; }
+    const int n = kKB * T * 64 * 8;
+    for (int idx = tid; idx < n; idx += 1024) {
+        const int i = idx & 7, l = (idx >> 3) & 63, t = (idx >> 9) % T, kb = (idx >> 9) / T;
+        const int m = 32 * t + (l & 31);
+        const int f = kperm(kb, l >> 5, i);
+        float w = 0.0f;
+        if (m < H && f >= 0) {
+            w = W1[(size_t)m * 198 + f];
+            if (f == 97 || f == 195) w = w / 15.0f;
+        }
+        _Float16 a, b;
+        split16(ldexpf(w, e1), a, b);
+        const size_t base = ((size_t)(kb * T + t) * 2) * 64 * 8;
+        w1q[base + (size_t)l * 8 + i] = a;
+        w1q[base + 64 * 8 + (size_t)l * 8 + i] = b;
     }
 }
 
@@ -291,26 +611,6 @@ __global__ void k_expand(Args A, const int32_t* lane_off, int32_t* row_lane) {
     const uint8_t* rr = A.lanes + (size_t)i * 64;
     const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
     for (int a = 0; a < n; ++a) row_lane[lane_off[i] + a] = i;
-}
-
-// Q(a) = sum_r p_r minv[a][r] (fp32, r in roll order), first argmax.
-__global__ void k_two_ply_reduce(Args A, const int32_t* lane_off, const float* minv, int32_t* best, float* bestq,
-                                 float* qout) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.B) return;
-    const uint8_t* rr = A.lanes + (size_t)i * 64;
-    const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
-    float bq = -INFINITY;
-    int ba = 0;
-    for (int a = 0; a < n; ++a) {
-        const float* mv = minv + ((size_t)lane_off[i] + a) * 21;
-        float q = 0.0f;
-        for (int r = 0; r < 21; ++r) q = fmaf(kRoll0[r] == kRoll1[r] ? 1.0f / 36.0f : 2.0f / 36.0f, mv[r], q);
-        if (qout) qout[(size_t)i * A.max_moves + a] = q;
-        if (q > bq) { bq = q; ba = a; }
-    }
-    best[i] = ba;
-    if (bestq) bestq[i] = n ? bq : 0.0f;
 }
 
 // 1-ply: every lane's afterstates a (mover's one-hot), first argmax V(a).
@@ -373,12 +673,22 @@ extern int bgx_internal_fail(hipError_t e);
 
 static int value_tiles(int H) { return H <= 32 ? 1 : 2; }
 
+template <typename K>
+static int persistent_grid(const bgx_engine* e, K kernel, int per_cu_cap) {
+    int cus = 0, occ = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 64, 0) != hipSuccess || occ <= 0) occ = 8;
+    if (occ > per_cu_cap) occ = per_cu_cap;
+    return cus * occ;
+}
+
 extern "C" {
 
 int bgx_value_packed_size(int32_t hidden) {
     if (hidden <= 0 || hidden > 64) return BGX_EINVAL;
     const int T = value_tiles(hidden);
-    return kK1 * T * 64 + 2 * T * 16 * 64 + 4;
+    return sz_f32(T) + sz_f16(T);
 }
 
 int bgx_value_pack(const float* W1, const float* b1, const float* wv, const float* bv, int32_t hidden, float* packed,
@@ -390,8 +700,13 @@ int bgx_value_pack(const float* W1, const float* b1, const float* wv, const floa
     float* b1p = w1p + kK1 * T * 64;
     float* wvp = b1p + T * 16 * 64;
     float* bvp = wvp + T * 16 * 64;
-    hipLaunchKernelGGL(k_value_pack, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream, W1, b1, wv, bv, hidden,
+    const int n32 = sz_f32(T);
+    hipLaunchKernelGGL(k_value_pack, dim3((n32 + 255) / 256), dim3(256), 0, (hipStream_t)stream, W1, b1, wv, bv, hidden,
                        T, w1p, b1p, wvp, bvp);
+    SCK(hipGetLastError());
+    float* f16s = packed + n32;
+    hipLaunchKernelGGL(k_value_pack16, dim3(1), dim3(1024), 0, (hipStream_t)stream, W1, hidden, T, (int*)f16s,
+                       (_Float16*)(f16s + 4));
     SCK(hipGetLastError());
     return BGX_OK;
 }
@@ -420,6 +735,8 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     return BGX_OK;
 }
 
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value_bias, int32_t* best_out,
                 float* bestq_out, float* q_out, uint64_t* stats_host, void* stream) {
     if (!e || !vpacked || !best_out || bgx_value_packed_size(hidden) < 0) return BGX_EINVAL;
@@ -427,28 +744,38 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     const size_t B = (size_t)A.B;
-    // workspace: [lane_off B i32][rows_total i64][leaves u64][slow_count i32 x4][slow_queue][row_lane][minv]
-    const size_t head = B * 4 + 64 + (size_t)kSlowQueue * 4;
-    if (e->search_ws_bytes < head) {
+    // workspace head: [lane_off B i32][counters 256 B][slow_queue]
+    struct Ctr { int64_t rows; unsigned long long leaves, cursor; int32_t slow_count, retry_count, list_count, pad; };
+    const size_t o_ctr = align256(B * 4), o_slow = o_ctr + 256, head = align256(o_slow + (size_t)kSlowQueue * 4);
+    auto grow = [&](size_t need) -> int {
+        if (e->search_ws_bytes >= need) return BGX_OK;
+        void* nw = nullptr;
+        SCK(hipStreamSynchronize(s));
+        SCK(hipMalloc(&nw, need + need / 4));
         if (e->search_ws) SCK(hipFree(e->search_ws));
-        e->search_ws = nullptr; e->search_ws_bytes = 0;
-        SCK(hipMalloc(&e->search_ws, head));
-        e->search_ws_bytes = head;
-    }
+        e->search_ws = nw;
+        e->search_ws_bytes = need + need / 4;
+        return BGX_OK;
+    };
+    int rc = grow(head);
+    if (rc != BGX_OK) return rc;
     char* ws = (char*)e->search_ws;
-    int32_t* lane_off = (int32_t*)ws;
-    int64_t* rows_total = (int64_t*)(ws + B * 4);
-    unsigned long long* leaves = (unsigned long long*)(ws + B * 4 + 8);
-    int32_t* slow_count = (int32_t*)(ws + B * 4 + 16);
-    SCK(hipMemsetAsync(ws + B * 4, 0, 64, s));
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, lane_off, rows_total);
+    SCK(hipMemsetAsync(ws + o_ctr, 0, 256, s));
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, (int32_t*)ws, (int64_t*)(ws + o_ctr));
     SCK(hipGetLastError());
-    int64_t rows = 0;
-    SCK(hipMemcpyAsync(&rows, rows_total, 8, hipMemcpyDeviceToHost, s));
+    int64_t rows64 = 0;
+    SCK(hipMemcpyAsync(&rows64, ws + o_ctr, 8, hipMemcpyDeviceToHost, s));
     SCK(hipStreamSynchronize(s));
-    const size_t need = head + (size_t)rows * 4 + (size_t)rows * 21 * 4 + 256;
+    const int64_t jobs64 = rows64 * 21;
+    if (jobs64 >= (int64_t)0x1FFFFFFF) return BGX_EINVAL;     // job ids are 29-bit pool tags
+    const int rows = (int)rows64, jobs = (int)jobs64;
+    // [row_lane rows][rowrec rows*64][rowside rows*16][minv jobs*4][maxlen jobs][list jobs*4][retry jobs*4]
+    const size_t o_rl = head, o_rec = align256(o_rl + (size_t)rows * 4), o_side = align256(o_rec + (size_t)rows * 64),
+                 o_minv = align256(o_side + (size_t)rows * 16), o_ml = align256(o_minv + (size_t)jobs * 4),
+                 o_list = align256(o_ml + (size_t)jobs), o_retry = align256(o_list + (size_t)jobs * 4),
+                 need = align256(o_retry + (size_t)jobs * 4);
     if (e->search_ws_bytes < need) {
-        // grow (keeps nothing: everything below is recomputed)
+        // keep the head (lane_off, counters) across the regrow
         void* nw = nullptr;
         SCK(hipMalloc(&nw, need + need / 4));
         SCK(hipMemcpyAsync(nw, e->search_ws, head, hipMemcpyDeviceToDevice, s));
@@ -457,37 +784,87 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         e->search_ws = nw;
         e->search_ws_bytes = need + need / 4;
         ws = (char*)nw;
-        lane_off = (int32_t*)ws;
-        rows_total = (int64_t*)(ws + B * 4);
-        leaves = (unsigned long long*)(ws + B * 4 + 8);
-        slow_count = (int32_t*)(ws + B * 4 + 16);
     }
-    int32_t* slow_queue = (int32_t*)(ws + B * 4 + 64);
-    int32_t* row_lane = (int32_t*)(ws + head);
-    float* minv = (float*)(ws + head + (((size_t)rows * 4 + 255) & ~(size_t)255));
-    hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
-    SearchArgs S{row_lane, lane_off, rows_total, minv, leaves, slow_count, slow_queue};
-    const VNet vn = make_vnet(vpacked, hidden, value_bias);
-    const int64_t njobs = rows * 21;
-    const int grid = (int)(njobs < 8192 ? (njobs > 0 ? njobs : 1) : 8192);
-    if (value_tiles(hidden) == 1) {
-        hipLaunchKernelGGL(k_two_ply<1>, dim3(grid), dim3(64), 0, s, A, S, vn);
-        hipLaunchKernelGGL(k_two_ply_slow<1>, dim3(e->slow_waves), dim3(64), 0, s, A, S, vn, e->slow_tables);
-    } else {
-        hipLaunchKernelGGL(k_two_ply<2>, dim3(grid), dim3(64), 0, s, A, S, vn);
-        hipLaunchKernelGGL(k_two_ply_slow<2>, dim3(e->slow_waves), dim3(64), 0, s, A, S, vn, e->slow_tables);
+    // leaf pool: ~32 slots per job (mean ~19 survivors at mid-game positions);
+    // BGX_2PLY_POOL overrides (tests force retry rounds with a tiny pool)
+    size_t cap = (size_t)jobs * 32 + kBlk * 64;
+    if (const char* ps = getenv("BGX_2PLY_POOL")) cap = (size_t)strtoull(ps, nullptr, 10);
+    cap = (cap + kBlk - 1) / kBlk * kBlk;
+    if (cap < (size_t)kBlk * 4) cap = (size_t)kBlk * 4;
+    if (cap > ((size_t)1 << 31)) cap = (size_t)1 << 31;
+    if (e->search_pool_cap < cap) {
+        SCK(hipStreamSynchronize(s));
+        if (e->search_pool) SCK(hipFree(e->search_pool));
+        e->search_pool = nullptr; e->search_pool_cap = 0;
+        SCK(hipMalloc(&e->search_pool, cap * 20));
+        e->search_pool_cap = cap;
     }
-    SCK(hipGetLastError());
+    const size_t pcap = e->search_pool_cap;
+    int32_t* lane_off = (int32_t*)ws;
+    Ctr* ctr = (Ctr*)(ws + o_ctr);
+    int32_t* row_lane = (int32_t*)(ws + o_rl);
+    uint8_t* rowrec = (uint8_t*)(ws + o_rec);
+    uint4* rowside = (uint4*)(ws + o_side);
+    int32_t* minv = (int32_t*)(ws + o_minv);
+    uint8_t* maxlen = (uint8_t*)(ws + o_ml);
+    int32_t* list = (int32_t*)(ws + o_list);
+    int32_t* retry = (int32_t*)(ws + o_retry);
+    uint4* keys = (uint4*)e->search_pool;
+    uint32_t* tags = (uint32_t*)(keys + pcap);
+
+    if (rows > 0) {
+        hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
+        SCK(hipMemsetAsync(minv, 0x7F, (size_t)jobs * 4, s));
+        SCK(hipMemsetAsync(maxlen, 0xFF, (size_t)jobs, s));
+        hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
+                           lane_off, rows, rowrec, rowside);
+        SCK(hipGetLastError());
+        S2 S{rowrec, rows, keys, tags, &ctr->cursor, (unsigned long long)pcap, maxlen, &ctr->leaves,
+             &ctr->slow_count, (int32_t*)(ws + o_slow), &ctr->retry_count, retry, list, &ctr->list_count, A.err,
+             cap_fast<kLogLight>(), cap_fast<10>()};
+        if (const char* fs = getenv("BGX_2PLY_LDS_CAP")) S.cap_light = S.cap_heavy = atoi(fs);   // tests: force the slow tier
+        const int T = value_tiles(hidden);
+        const float* f16s = vpacked + sz_f32(T);
+        const VNet vn = make_vnet(vpacked, hidden, value_bias);
+        EvalArgs E{keys, tags, &ctr->cursor, (unsigned long long)pcap, rowside, maxlen, minv,
+                   (const uint4*)(f16s + 4), vn.b1p, vn.wvp, (const int*)f16s, value_bias};
+        const int g_light = persistent_grid(e, k_enum<kLogLight, false, 0>, 32);
+        const int g_heavy = persistent_grid(e, k_enum<10, true, 1>, 32);
+        const int g_list = persistent_grid(e, k_enum<10, true, 2>, 32);
+        const int g_eval = persistent_grid(e, T == 1 ? k_eval<1> : k_eval<2>, 16);
+        for (int round = 0;; ++round) {
+            if (round == 0) {
+                hipLaunchKernelGGL((k_enum<10, true, 1>), dim3(g_heavy), dim3(64), 0, s, S);
+                hipLaunchKernelGGL((k_enum<kLogLight, false, 0>), dim3(g_light), dim3(64), 0, s, S);
+            } else {
+                hipLaunchKernelGGL((k_enum<10, true, 2>), dim3(g_list), dim3(64), 0, s, S);
+            }
+            hipLaunchKernelGGL(k_enum_slow, dim3(e->slow_waves), dim3(64), 0, s, S, e->slow_tables);
+            if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64), 0, s, E);
+            else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64), 0, s, E);
+            SCK(hipGetLastError());
+            int32_t nretry = 0;
+            SCK(hipMemcpyAsync(&nretry, &ctr->retry_count, 4, hipMemcpyDeviceToHost, s));
+            SCK(hipStreamSynchronize(s));
+            if (nretry == 0) break;
+            if (round + 1 >= kMaxRounds) return BGX_ENOMEM;
+            // next round: the lost jobs become the explicit list, the pool starts over
+            SCK(hipMemcpyAsync(list, retry, (size_t)nretry * 4, hipMemcpyDeviceToDevice, s));
+            SCK(hipMemcpyAsync(&ctr->list_count, &ctr->retry_count, 4, hipMemcpyDeviceToDevice, s));
+            SCK(hipMemsetAsync(&ctr->cursor, 0, 8, s));
+            SCK(hipMemsetAsync(&ctr->slow_count, 0, 8, s));      // slow_count and retry_count
+        }
+    }
     hipLaunchKernelGGL(k_two_ply_reduce, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, minv, best_out,
                        bestq_out, q_out);
     SCK(hipGetLastError());
     if (stats_host) {
         unsigned long long lv = 0;
-        SCK(hipMemcpyAsync(&lv, leaves, 8, hipMemcpyDeviceToHost, s));
+        SCK(hipMemcpyAsync(&lv, &ctr->leaves, 8, hipMemcpyDeviceToHost, s));
         SCK(hipStreamSynchronize(s));
         stats_host[0] = lv;
-        stats_host[1] = (uint64_t)njobs;
-        stats_host[2] = (uint64_t)rows;
+        stats_host[1] = (uint64_t)jobs64;
+        stats_host[2] = (uint64_t)rows64;
     }
     return BGX_OK;
 }

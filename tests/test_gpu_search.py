@@ -91,3 +91,37 @@ def test_two_ply_vs_oracle_composition(setup):
     assert checked == 10
     assert stats["leaves"] == leaves
     assert stats["afterstates"] == int(n_all.sum()) and stats["jobs"] == 21 * int(n_all.sum())
+
+
+def test_two_ply_pool_retry_rounds(setup, monkeypatch):
+    """A leaf pool far too small for one pass: lost jobs are re-run in later
+    rounds; Q, the choice and the exact leaf count must not change."""
+    bgx, net, vh, eng = setup
+    from bgx.search import two_ply
+    best, bestq, q, st = two_ply(eng, vh, want_q=True)
+    monkeypatch.setenv("BGX_2PLY_POOL", "32768")
+    best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
+    assert st2["leaves"] == st["leaves"]
+    assert torch.equal(torch.nan_to_num(q2, 7.0), torch.nan_to_num(q, 7.0))
+    assert torch.equal(best2, best) and torch.equal(bestq2, bestq)
+
+
+def test_two_ply_slow_tier(setup, monkeypatch):
+    """Every reply enumeration forced through the HBM-table tier (tiny LDS
+    capacity): same Q and leaf count as the LDS path, checked against the oracle."""
+    bgx, net, vh, _ = setup
+    from bgx.search import two_ply
+    eng = bgx.Engine(batch=3, max_moves=500, dice="mt", auto_reset=True)
+    eng.seed(np.arange(900, 903, dtype=np.uint32))
+    eng.reset()
+    rng = np.random.RandomState(5)
+    for _ in range(12):
+        nm = eng.n_moves().cpu().numpy()
+        eng.step(torch.from_numpy(np.array([rng.randint(k) if k else 0 for k in nm], np.int32)).cuda())
+    best, bestq, q, st = two_ply(eng, vh, want_q=True)
+    monkeypatch.setenv("BGX_2PLY_LDS_CAP", "6")
+    best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
+    assert eng.error() == 0
+    assert st2["leaves"] == st["leaves"]
+    assert torch.equal(torch.nan_to_num(q2, 7.0), torch.nan_to_num(q, 7.0))
+    assert torch.equal(best2, best)
