@@ -13,7 +13,8 @@
 //             tag (job, sub-move count) streamed to an HBM leaf pool in 256-slot
 //             blocks; three variants: non-doubles rolls (4 KiB of LDS, no doubles
 //             code), doubles rolls (dedup table + memo), and an explicit job list;
-//   k_enum_slow  jobs whose dedup set outgrew LDS, on 2 MiB HBM tables;
+//   k_enum_tier  jobs whose dedup set outgrew their table: 1,024- then 4,096-slot LDS tables;
+//   k_enum_slow  jobs that outgrew that too, on 131,072-slot HBM tables;
 //   k_eval    dense pass over the pool: features from (row side, key) as exact
 //             f16 values, W1 split hi+lo on v_mfma_f32_32x32x16_f16, value head
 //             in registers, segmented min per job + atomicMin into minv[job];
@@ -27,6 +28,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdio.h>
+#include <string.h>
 
 #include "bg_engine.h"
 
@@ -170,14 +173,14 @@ struct S2 {
     unsigned long long cap;
     uint8_t* maxlen;                  // [jobs] final max sub-move count (0xFF = not finished)
     unsigned long long* leaves;       // surviving-leaf counter (stats)
-    int32_t* slow_count;
-    int32_t* slow_queue;              // [kSlowQueue]
+    int32_t* qcount;                  // [kTiers] overflow queues: 0 -> 1,024-slot LDS tier,
+    int32_t* queues;                  // [kTiers][kSlowQueue]   1 -> 4,096-slot LDS tier, 2 -> HBM tier
     int32_t* retry_count;
     int32_t* retry_list;              // [jobs]
     const int32_t* list;              // explicit job list (variant 2)
     const int32_t* list_count;
     int32_t* err;
-    int cap_light, cap_heavy;         // unique-entry capacity of the LDS tables (tests shrink them)
+    int cap_light, cap_heavy, cap_mid;   // unique-entry capacity of the LDS tables (tests shrink them)
 };
 
 __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
@@ -235,7 +238,8 @@ struct KeySink {
 
 // One (row, roll) job.  KIND 0: non-doubles roll, 1: doubles roll, 2: either.
 // Returns 0 done, 1 LDS/HBM table overflow, 2 pool exhausted.
-template <int LOG, typename SlotPtr, bool MEMO, int KIND>
+// MK: revisit memo kind (-1 none, 0 separate depth-2/3 tables, 1 one combined table).
+template <int LOG, typename SlotPtr, int MK, int KIND>
 __device__ __forceinline__ int enum_job(const S2& S, int job, SlotPtr tab, int cap_unique, uint4* memo,
                                         KeySink& sink, unsigned long long& leaves) {
     const int row = job / 21, r = job - row * 21;
@@ -247,13 +251,14 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, SlotPtr tab, int c
     const Node sq = node_from_bytes(bv, q, blocked);
     for (int i = l; i < (1 << LOG); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = KIND == 1 || (KIND == 2 && r0 == r1);
-    if (MEMO && dbl)
-        for (int i = l; i < kMemoSlots; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
+    constexpr int kMemoN = MK == 1 ? (1 << kLogCMemo) : kMemoSlots;
+    if (MK >= 0 && dbl)
+        for (int i = l; i < kMemoN; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    Gen<LOG, SlotPtr, KeySink> g;
+    Gen<LOG, SlotPtr, KeySink, MK < 0 ? 0 : MK> g;
     g.tab = tab; g.pl = q; g.cap_unique = cap_unique; g.blocked = blocked;
-    g.memo2 = MEMO && dbl ? memo : nullptr;
-    g.memo3 = MEMO && dbl ? memo + (1 << kLogMemo2) : nullptr;
+    g.memo2 = MK >= 0 && dbl ? memo : nullptr;
+    g.memo3 = MK >= 0 && dbl ? (MK == 1 ? memo : memo + (1 << kLogMemo2)) : nullptr;
     g.sink = sink;
     g.sink.job = (uint32_t)job;
     g.sink.lost = false;
@@ -287,11 +292,11 @@ __device__ __forceinline__ KeySink make_sink(const S2& S) {
 
 // VARIANT 0: jobs (row, non-doubles roll) implicit, 1: (row, doubles roll)
 // implicit, 2: the explicit list.
-template <int LOG, bool MEMO, int VARIANT>
+template <int LOG, int MK, int VARIANT>
 __global__ __launch_bounds__(64) void k_enum(S2 S) {
     __shared__ uint4 tab[1 << LOG];
-    __shared__ uint4 memo_[MEMO ? kMemoSlots : 1];
-    uint4* memo = MEMO ? memo_ : nullptr;
+    __shared__ uint4 memo_[MK == 0 ? kMemoSlots : (MK == 1 ? (1 << kLogCMemo) : 1)];
+    uint4* memo = MK >= 0 ? memo_ : nullptr;
     KeySink sink = make_sink(S);
     unsigned long long leaves = 0;
     const int64_t n = VARIANT == 0 ? (int64_t)S.rows * 15 : VARIANT == 1 ? (int64_t)S.rows * 6 : *S.list_count;
@@ -300,25 +305,51 @@ __global__ __launch_bounds__(64) void k_enum(S2 S) {
         if (VARIANT == 0) { const int row = (int)(i / 15); job = row * 21 + kNdRoll[i - (int64_t)row * 15]; }
         else if (VARIANT == 1) { const int row = (int)(i / 6); job = row * 21 + kDbRoll[i - (int64_t)row * 6]; }
         else job = S.list[i];
-        const int st = enum_job<LOG, uint4*, MEMO, VARIANT>(S, job, tab, VARIANT == 0 ? S.cap_light : S.cap_heavy, memo,
+        const int st = enum_job<LOG, uint4*, MK, VARIANT>(S, job, tab, VARIANT == 0 ? S.cap_light : S.cap_heavy, memo,
                                                              sink, leaves);
-        if (st == 1) queue_job(S.slow_count, S.slow_queue, kSlowQueue, job, S.retry_count, S.retry_list);
+        if (st == 1) {
+            const int qo = LOG < 10 ? 0 : 1;
+            queue_job(S.qcount + qo, S.queues + (size_t)qo * kSlowQueue, kSlowQueue, job, S.retry_count, S.retry_list);
+        }
         else if (st == 2) queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
     }
     sink.finish();
     if (lane_id() == 0 && leaves) atomicAdd(S.leaves, leaves);
 }
 
-// Jobs whose dedup set outgrew the LDS table: 131,072-slot HBM table per wave.
+// Overflow tiers in LDS: queue QI (jobs whose dedup set outgrew their table) on a
+// 2^LOG-slot table; what outgrows it too goes to queue QI + 1.
+constexpr int kLogMid = 12;
+template <int LOG, int QI>
+__global__ __launch_bounds__(64) void k_enum_tier(S2 S) {
+    __shared__ uint4 tab[1 << LOG];
+    __shared__ uint4 memo[kMemoSlots];
+    KeySink sink = make_sink(S);
+    unsigned long long leaves = 0;
+    const int n = min(S.qcount[QI], kSlowQueue);
+    const int32_t* qin = S.queues + (size_t)QI * kSlowQueue;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int job = qin[i];
+        const int st = enum_job<LOG, uint4*, 0, 2>(S, job, tab, min(S.cap_mid, cap_fast<LOG>()), memo,
+                                                   sink, leaves);
+        if (st == 1) queue_job(S.qcount + QI + 1, S.queues + (size_t)(QI + 1) * kSlowQueue, kSlowQueue, job,
+                               S.retry_count, S.retry_list);
+        else if (st == 2) queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
+    }
+    sink.finish();
+    if (lane_id() == 0 && leaves) atomicAdd(S.leaves, leaves);
+}
+
+// Tier 2: a 131,072-slot HBM table per wave.
 __global__ __launch_bounds__(64) void k_enum_slow(S2 S, uint4* tables) {
     __shared__ uint4 memo[kMemoSlots];
     uint4* tab = tables + ((size_t)blockIdx.x << kLogSlotsSlow);
     KeySink sink = make_sink(S);
     unsigned long long leaves = 0;
-    const int n = min(*S.slow_count, kSlowQueue);
+    const int n = min(S.qcount[2], kSlowQueue);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
-        const int job = S.slow_queue[i];
-        const int st = enum_job<kLogSlotsSlow, uint4*, true, 2>(S, job, tab, kCapSlow, memo, sink, leaves);
+        const int job = S.queues[2 * (size_t)kSlowQueue + i];
+        const int st = enum_job<kLogSlotsSlow, uint4*, 0, 2>(S, job, tab, kCapSlow, memo, sink, leaves);
         if (st == 1 && lane_id() == 0) atomicOr(S.err, 1);
         else if (st == 2) queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
     }
@@ -744,9 +775,9 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     const size_t B = (size_t)A.B;
-    // workspace head: [lane_off B i32][counters 256 B][slow_queue]
-    struct Ctr { int64_t rows; unsigned long long leaves, cursor; int32_t slow_count, retry_count, list_count, pad; };
-    const size_t o_ctr = align256(B * 4), o_slow = o_ctr + 256, head = align256(o_slow + (size_t)kSlowQueue * 4);
+    // workspace head: [lane_off B i32][counters 256 B][overflow queues]
+    struct Ctr { int64_t rows; unsigned long long leaves, cursor; int32_t qcount[3], retry_count, list_count; };
+    const size_t o_ctr = align256(B * 4), o_q = o_ctr + 256, head = align256(o_q + (size_t)3 * kSlowQueue * 4);
     auto grow = [&](size_t need) -> int {
         if (e->search_ws_bytes >= need) return BGX_OK;
         void* nw = nullptr;
@@ -785,21 +816,6 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         e->search_ws_bytes = need + need / 4;
         ws = (char*)nw;
     }
-    // leaf pool: ~32 slots per job (mean ~19 survivors at mid-game positions);
-    // BGX_2PLY_POOL overrides (tests force retry rounds with a tiny pool)
-    size_t cap = (size_t)jobs * 32 + kBlk * 64;
-    if (const char* ps = getenv("BGX_2PLY_POOL")) cap = (size_t)strtoull(ps, nullptr, 10);
-    cap = (cap + kBlk - 1) / kBlk * kBlk;
-    if (cap < (size_t)kBlk * 4) cap = (size_t)kBlk * 4;
-    if (cap > ((size_t)1 << 31)) cap = (size_t)1 << 31;
-    if (e->search_pool_cap < cap) {
-        SCK(hipStreamSynchronize(s));
-        if (e->search_pool) SCK(hipFree(e->search_pool));
-        e->search_pool = nullptr; e->search_pool_cap = 0;
-        SCK(hipMalloc(&e->search_pool, cap * 20));
-        e->search_pool_cap = cap;
-    }
-    const size_t pcap = e->search_pool_cap;
     int32_t* lane_off = (int32_t*)ws;
     Ctr* ctr = (Ctr*)(ws + o_ctr);
     int32_t* row_lane = (int32_t*)(ws + o_rl);
@@ -809,8 +825,6 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     uint8_t* maxlen = (uint8_t*)(ws + o_ml);
     int32_t* list = (int32_t*)(ws + o_list);
     int32_t* retry = (int32_t*)(ws + o_retry);
-    uint4* keys = (uint4*)e->search_pool;
-    uint32_t* tags = (uint32_t*)(keys + pcap);
 
     if (rows > 0) {
         hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
@@ -819,40 +833,83 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
                            lane_off, rows, rowrec, rowside);
         SCK(hipGetLastError());
-        S2 S{rowrec, rows, keys, tags, &ctr->cursor, (unsigned long long)pcap, maxlen, &ctr->leaves,
-             &ctr->slow_count, (int32_t*)(ws + o_slow), &ctr->retry_count, retry, list, &ctr->list_count, A.err,
-             cap_fast<kLogLight>(), cap_fast<10>()};
-        if (const char* fs = getenv("BGX_2PLY_LDS_CAP")) S.cap_light = S.cap_heavy = atoi(fs);   // tests: force the slow tier
+        S2 S{rowrec, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
+             ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
+             retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>()};
+        // doubles enumerator: dedup table 2^LOG slots + revisit memo kind (BGX_2PLY_HEAVY=LOG:MK)
+        int hlog = 9, hmk = 0;
+        if (const char* hv = getenv("BGX_2PLY_HEAVY")) { hlog = atoi(hv); const char* c = strchr(hv, ':'); if (c) hmk = atoi(c + 1); }
+        void (*kheavy)(S2) = k_enum<9, 0, 1>;
+        void (*klist)(S2) = k_enum<9, 0, 2>;
+        if (hlog == 8 && hmk == 0) { kheavy = k_enum<8, 0, 1>; klist = k_enum<8, 0, 2>; }
+        else if (hlog == 10 && hmk == 0) { kheavy = k_enum<10, 0, 1>; klist = k_enum<10, 0, 2>; }
+        else if (hlog == 9 && hmk == 1) { kheavy = k_enum<9, 1, 1>; klist = k_enum<9, 1, 2>; }
+        else hlog = 9;
+        S.cap_heavy = (7 << hlog) / 8;
+        if (const char* fs = getenv("BGX_2PLY_LDS_CAP")) {    // tests: force the overflow tiers ("first[:mid]")
+            S.cap_light = S.cap_heavy = S.cap_mid = atoi(fs);
+            if (const char* c = strchr(fs, ':')) S.cap_mid = atoi(c + 1);
+        }
+        const bool dbg = getenv("BGX_2PLY_DEBUG") != nullptr;
         const int T = value_tiles(hidden);
         const float* f16s = vpacked + sz_f32(T);
         const VNet vn = make_vnet(vpacked, hidden, value_bias);
-        EvalArgs E{keys, tags, &ctr->cursor, (unsigned long long)pcap, rowside, maxlen, minv,
+        EvalArgs E{nullptr, nullptr, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), vn.b1p, vn.wvp, (const int*)f16s, value_bias};
-        const int g_light = persistent_grid(e, k_enum<kLogLight, false, 0>, 32);
-        const int g_heavy = persistent_grid(e, k_enum<10, true, 1>, 32);
-        const int g_list = persistent_grid(e, k_enum<10, true, 2>, 32);
+        const int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
+        const int g_heavy = persistent_grid(e, kheavy, 32);
+        const int g_list = persistent_grid(e, klist, 32);
+        const int g_t0 = persistent_grid(e, k_enum_tier<10, 0>, 32);
+        const int g_mid = persistent_grid(e, k_enum_tier<kLogMid, 1>, 32);
+        // leaf pool: ~32 slots per job (mean ~19 survivors at mid-game positions);
+        // BGX_2PLY_POOL overrides (tests force retry rounds with a tiny pool)
+        // every resident wave may hold a partly filled block in each tier
+        size_t cap = (size_t)jobs * 32 + (size_t)(g_light + g_heavy + g_list + g_t0 + g_mid + e->slow_waves) * kBlk * 2;
+        if (const char* ps = getenv("BGX_2PLY_POOL")) cap = (size_t)strtoull(ps, nullptr, 10);
+        cap = (cap + kBlk - 1) / kBlk * kBlk;
+        if (cap < (size_t)kBlk * 4) cap = (size_t)kBlk * 4;
+        if (cap > ((size_t)1 << 31)) cap = (size_t)1 << 31;
+        if (e->search_pool_cap < cap) {
+            SCK(hipStreamSynchronize(s));
+            if (e->search_pool) SCK(hipFree(e->search_pool));
+            e->search_pool = nullptr; e->search_pool_cap = 0;
+            SCK(hipMalloc(&e->search_pool, cap * 20));
+            e->search_pool_cap = cap;
+        }
+        const size_t pcap = e->search_pool_cap;
+        S.keys = (uint4*)e->search_pool;
+        S.tags = (uint32_t*)(S.keys + pcap);
+        E.keys = S.keys;
+        E.tags = S.tags;
+        S.cap = E.cap = (unsigned long long)pcap;
         const int g_eval = persistent_grid(e, T == 1 ? k_eval<1> : k_eval<2>, 16);
         for (int round = 0;; ++round) {
             if (round == 0) {
-                hipLaunchKernelGGL((k_enum<10, true, 1>), dim3(g_heavy), dim3(64), 0, s, S);
-                hipLaunchKernelGGL((k_enum<kLogLight, false, 0>), dim3(g_light), dim3(64), 0, s, S);
+                hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
             } else {
-                hipLaunchKernelGGL((k_enum<10, true, 2>), dim3(g_list), dim3(64), 0, s, S);
+                hipLaunchKernelGGL(klist, dim3(g_list), dim3(64), 0, s, S);
             }
+            hipLaunchKernelGGL((k_enum_tier<10, 0>), dim3(g_t0), dim3(64), 0, s, S);
+            hipLaunchKernelGGL((k_enum_tier<kLogMid, 1>), dim3(g_mid), dim3(64), 0, s, S);
             hipLaunchKernelGGL(k_enum_slow, dim3(e->slow_waves), dim3(64), 0, s, S, e->slow_tables);
             if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64), 0, s, E);
             else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64), 0, s, E);
             SCK(hipGetLastError());
-            int32_t nretry = 0;
-            SCK(hipMemcpyAsync(&nretry, &ctr->retry_count, 4, hipMemcpyDeviceToHost, s));
+            Ctr hc;
+            SCK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, s));
             SCK(hipStreamSynchronize(s));
+            const int32_t nretry = hc.retry_count;
+            if (dbg)
+                fprintf(stderr, "[bgx 2-ply] round %d: pool %llu/%zu, tier1 %d, tier2 %d, retry %d, leaves %llu\n", round,
+                        hc.cursor, pcap, hc.qcount[0] + hc.qcount[1], hc.qcount[2], hc.retry_count, hc.leaves);
             if (nretry == 0) break;
             if (round + 1 >= kMaxRounds) return BGX_ENOMEM;
             // next round: the lost jobs become the explicit list, the pool starts over
             SCK(hipMemcpyAsync(list, retry, (size_t)nretry * 4, hipMemcpyDeviceToDevice, s));
             SCK(hipMemcpyAsync(&ctr->list_count, &ctr->retry_count, 4, hipMemcpyDeviceToDevice, s));
             SCK(hipMemsetAsync(&ctr->cursor, 0, 8, s));
-            SCK(hipMemsetAsync(&ctr->slow_count, 0, 8, s));      // slow_count and retry_count
+            SCK(hipMemsetAsync(ctr->qcount, 0, 16, s));          // qcount[3], retry_count
         }
     }
     hipLaunchKernelGGL(k_two_ply_reduce, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, minv, best_out,

@@ -106,9 +106,12 @@ def test_two_ply_pool_retry_rounds(setup, monkeypatch):
     assert torch.equal(best2, best) and torch.equal(bestq2, bestq)
 
 
-def test_two_ply_slow_tier(setup, monkeypatch):
-    """Every reply enumeration forced through the HBM-table tier (tiny LDS
-    capacity): same Q and leaf count as the LDS path, checked against the oracle."""
+@pytest.mark.parametrize("caps", ["6:3584", "6"])
+@pytest.mark.parametrize("heavy", ["9:0", "10:0"])
+def test_two_ply_overflow_tiers(setup, monkeypatch, caps, heavy):
+    """Every reply enumeration forced out of its first LDS table: into the
+    4,096-slot LDS tier ("6:3584") or on through it to the HBM-table tier ("6").
+    Same Q, choice and leaf count as the normal path."""
     bgx, net, vh, _ = setup
     from bgx.search import two_ply
     eng = bgx.Engine(batch=3, max_moves=500, dice="mt", auto_reset=True)
@@ -119,7 +122,8 @@ def test_two_ply_slow_tier(setup, monkeypatch):
         nm = eng.n_moves().cpu().numpy()
         eng.step(torch.from_numpy(np.array([rng.randint(k) if k else 0 for k in nm], np.int32)).cuda())
     best, bestq, q, st = two_ply(eng, vh, want_q=True)
-    monkeypatch.setenv("BGX_2PLY_LDS_CAP", "6")
+    monkeypatch.setenv("BGX_2PLY_HEAVY", heavy)
+    monkeypatch.setenv("BGX_2PLY_LDS_CAP", caps)
     best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
     assert eng.error() == 0
     assert st2["leaves"] == st["leaves"]
