@@ -415,15 +415,25 @@ struct EvalArgs {
     float bv;
 };
 
-__device__ __forceinline__ Leaf load_leaf(const EvalArgs& E, unsigned long long i) {
-    const uint4 key = E.keys[i];
-    const uint32_t tag = E.tags[i];
+struct LeafRaw { uint4 key; uint32_t tag; };
+struct LeafRow { uint4 rs; uint32_t ml; };
+
+__device__ __forceinline__ LeafRaw load_raw(const EvalArgs& E, unsigned long long i) {
+    return LeafRaw{E.keys[i], E.tags[i]};
+}
+__device__ __forceinline__ LeafRow load_row(const EvalArgs& E, const LeafRaw& r) {
+    const int job = r.tag != kTagNone ? (int)(r.tag & 0x1FFFFFFFu) : 0;
+    return LeafRow{E.rowside[job / 21], (uint32_t)E.maxlen[job]};
+}
+
+// Both sides of the reply afterstate: the replier q's from the key, the root
+// mover's = its side of a minus the blots q hit (a hit point held exactly one).
+__device__ __forceinline__ Leaf make_leaf(const LeafRaw& r, const LeafRow& w) {
+    const uint4 key = r.key, rs = w.rs;
     Leaf L;
-    const bool used = tag != kTagNone;
-    const int job = used ? (int)(tag & 0x1FFFFFFFu) : 0;
-    const uint4 rs = E.rowside[job / 21];
-    L.valid = used && (uint32_t)E.maxlen[job] == (tag >> 29);
-    L.job = L.valid ? job : -1;
+    const bool used = r.tag != kTagNone;
+    L.valid = used && w.ml == (r.tag >> 29);
+    L.job = L.valid ? (int)(r.tag & 0x1FFFFFFFu) : -1;
     const uint32_t hits = key.w >> 8;
     const uint64_t mlo = (((uint64_t)rs.y << 32) | rs.x) - spread4(hits & 0xFFFFu);
     const uint32_t mhi = rs.z - (uint32_t)spread4(hits >> 16);
@@ -479,27 +489,46 @@ __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0
 // fragments): X1s = W1s . F^T + b1 2^e1 on v_mfma_f32_32x32x16_f16 (hi and lo
 // parts of W1s, features exact), V = wv . relu(X1s 2^-e1) + bv, then per job the
 // min over its leaves (leaves of a job are contiguous in the pool).
+// Workgroup = 4 waves sharing the packed weights in LDS (T = 2: 53 KiB of W1
+// fragments + 16 KiB of bias / value-head lanes); every wave walks its own tiles
+// with the next tile's pool entries in flight during the current tile's MFMAs.
+constexpr int kEvalWaves = 4;
 template <int T>
-__global__ __launch_bounds__(64) void k_eval(EvalArgs E) {
+__global__ __launch_bounds__(64 * kEvalWaves) void k_eval(EvalArgs E) {
+    __shared__ uint4 wq[kKB * T * 2 * 64];
+    __shared__ float2 bw[T * 16 * 64];
     const int l = lane_id(), h = l >> 5, c = l & 31;
-    const unsigned long long used = *E.cursor < E.cap ? *E.cursor : E.cap;
-    const unsigned long long tiles = used / 64;
     const int e1 = E.hdr[0];
     const float up = ldexpf(1.0f, e1), down = ldexpf(1.0f, -e1);
-    for (unsigned long long tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    for (int i = threadIdx.x; i < kKB * T * 2 * 64; i += blockDim.x) wq[i] = E.w1q[i];
+    for (int i = threadIdx.x; i < T * 16 * 64; i += blockDim.x) bw[i] = make_float2(E.b1p[i] * up, E.wvp[i]);
+    __syncthreads();
+    const unsigned long long used = *E.cursor < E.cap ? *E.cursor : E.cap;
+    const unsigned long long tiles = used / 64;
+    const unsigned long long stride = (unsigned long long)gridDim.x * kEvalWaves;
+    unsigned long long tile = (unsigned long long)blockIdx.x * kEvalWaves + (threadIdx.x >> 6);
+    if (tile >= tiles) return;
+    LeafRaw raw[2];
+    LeafRow row[2];
+    #pragma unroll
+    for (int n = 0; n < 2; ++n) { raw[n] = load_raw(E, tile * 64 + 32 * n + c); row[n] = load_row(E, raw[n]); }
+    for (; tile < tiles; tile += stride) {
         Leaf L[2];
         #pragma unroll
-        for (int n = 0; n < 2; ++n) L[n] = load_leaf(E, tile * 64 + 32 * n + c);
-        // re-read the weight fragments every tile (L1/L2 hits) instead of letting
-        // the compiler hoist all 52 of them into 208 registers (1 wave per SIMD)
-        const uint4* w1q = E.w1q;
-        __asm__ volatile("" : "+s"(w1q));
+        for (int n = 0; n < 2; ++n) L[n] = make_leaf(raw[n], row[n]);
+        // an opaque zero offset per tile keeps the LDS fragment reads inside the loop
+        // (hoisted, the 52 fragments would take 208 registers: one wave per SIMD)
+        int z = 0;
+        __asm__ volatile("" : "+s"(z));
+        const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
         f32x16 x[2][T];
         #pragma unroll
         for (int t = 0; t < T; ++t)
             #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float b = E.b1p[(t * 16 + r) * 64 + l] * up;
+                const float b = bw[(t * 16 + r) * 64 + l + z].x;
                 x[0][t][r] = b;
                 x[1][t][r] = b;
             }
@@ -508,8 +537,8 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs E) {
             const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
             #pragma unroll
             for (int t = 0; t < T; ++t) {
-                const f16x8 ah = __builtin_bit_cast(f16x8, w1q[((kb * T + t) * 2 + 0) * 64 + l]);
-                const f16x8 al = __builtin_bit_cast(f16x8, w1q[((kb * T + t) * 2 + 1) * 64 + l]);
+                const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * T + t) * 2 + 0) * 64 + l + z]);
+                const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * T + t) * 2 + 1) * 64 + l + z]);
                 x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f0, x[0][t], 0, 0, 0);
                 x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f1, x[1][t], 0, 0, 0);
                 x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, x[0][t], 0, 0, 0);
@@ -517,15 +546,18 @@ __global__ __launch_bounds__(64) void k_eval(EvalArgs E) {
             }
         }
         #pragma unroll
+        for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
+        #pragma unroll
         for (int n = 0; n < 2; ++n) {
             float v = 0.0f;
             #pragma unroll
             for (int t = 0; t < T; ++t)
                 #pragma unroll
-                for (int r = 0; r < 16; ++r) v = fmaf(fmaxf(x[n][t][r] * down, 0.0f), E.wvp[(t * 16 + r) * 64 + l], v);
+                for (int r = 0; r < 16; ++r)
+                    v = fmaf(fmaxf(x[n][t][r] * down, 0.0f), bw[(t * 16 + r) * 64 + l + z].y, v);
             v += __shfl_xor(v, 32);
             v += E.bv;
-            int jb = L[n].job;
+            const int jb = L[n].job;
             v = L[n].valid ? v : INFINITY;
             // segmented min over equal-job runs of the 32 columns (lanes 0..31 == 32..63)
             #pragma unroll
@@ -882,7 +914,10 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         E.keys = S.keys;
         E.tags = S.tags;
         S.cap = E.cap = (unsigned long long)pcap;
-        const int g_eval = persistent_grid(e, T == 1 ? k_eval<1> : k_eval<2>, 16);
+        int g_eval = 0, ncu = 0;
+        SCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device));
+        SCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&g_eval, T == 1 ? k_eval<1> : k_eval<2>, 64 * kEvalWaves, 0));
+        g_eval = (g_eval > 0 ? g_eval : 1) * (ncu > 0 ? ncu : 256);
         for (int round = 0;; ++round) {
             if (round == 0) {
                 hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
@@ -893,8 +928,8 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             hipLaunchKernelGGL((k_enum_tier<10, 0>), dim3(g_t0), dim3(64), 0, s, S);
             hipLaunchKernelGGL((k_enum_tier<kLogMid, 1>), dim3(g_mid), dim3(64), 0, s, S);
             hipLaunchKernelGGL(k_enum_slow, dim3(e->slow_waves), dim3(64), 0, s, S, e->slow_tables);
-            if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64), 0, s, E);
-            else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64), 0, s, E);
+            if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64 * kEvalWaves), 0, s, E);
+            else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64 * kEvalWaves), 0, s, E);
             SCK(hipGetLastError());
             Ctr hc;
             SCK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, s));
