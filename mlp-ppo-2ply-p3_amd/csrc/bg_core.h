@@ -335,6 +335,7 @@ constexpr int kLogCMemo = 9;      // MEMO_KIND 1: depth-2 and depth-3 entries sh
 // Where surviving entries go.  MoveSink: the env's ordered move list in HBM
 // (first `cap` entries).  Other sinks (bg_search.hip) keep afterstate keys.
 struct MoveSink {
+    static constexpr bool kEnc = true;     // needs the move encodings
     uint64_t* out;      // this game's move list, `cap` entries
     int cap;
     __device__ __forceinline__ void reset() {}
@@ -391,7 +392,7 @@ struct Gen {
         if (act) {
             const Sub m = child(s, k, l, d, pl);
             t = apply(s, m, pl);
-            enc = m.enc;
+            enc = Sink::kEnc ? m.enc : 0u;
         }
         return act;
     }
@@ -463,7 +464,7 @@ struct Gen {
             const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
             const Node s = shfl_node(t, src);
             const Kids k{qb, __shfl(x, src)};
-            const uint64_t pe = (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc, src) |
+            const uint64_t pe = !Sink::kEnc ? 0ull : (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc, src) |
                                 ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(penc >> 32), src) << 32);
             Node leaf;
             uint64_t enc = 0;
@@ -472,7 +473,7 @@ struct Gen {
             if (valid) {
                 const Sub m = child(s, k, select_bit(qb, j), d, pl);
                 leaf = apply(s, m, pl);
-                enc = pe | ((uint64_t)m.enc << shift);
+                enc = Sink::kEnc ? pe | ((uint64_t)m.enc << shift) : 0ull;
                 found = probe_lane<LOG_SLOTS>(tab, (uint32_t)leaf.lo, (uint32_t)(leaf.lo >> 32), leaf.hi, leaf.k3, slot);
             }
             commit<true>(__ballot(valid && !found), leaf, enc, slot, len);
@@ -561,14 +562,14 @@ struct Gen {
             const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
             const Node s2 = shfl_node(t2, src);
             const Kids k{qb, __shfl(x3, src)};
-            const uint64_t pe = (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc2, src) |
+            const uint64_t pe = !Sink::kEnc ? 0ull : (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc2, src) |
                                 ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(penc2 >> 32), src) << 32);
             Node t3;
             uint64_t pe3 = 0;
             if (valid) {
                 const Sub m = child(s2, k, select_bit(qb, j), d, pl);
                 t3 = apply(s2, m, pl);
-                pe3 = pe | ((uint64_t)m.enc << 32);
+                pe3 = Sink::kEnc ? pe | ((uint64_t)m.enc << 32) : 0ull;
             }
             const uint64_t f3 = memo_batch<kLogMemo3, true>(memo3, n_memo3, valid, t3, kTag3);
             uint32_t q4 = 0;
@@ -609,13 +610,13 @@ struct Gen {
             const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
             const Node s1 = shfl_node(t1, src);
             const Kids k{qb, __shfl(x2, src)};
-            const uint64_t pe = (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc1, src);
+            const uint64_t pe = !Sink::kEnc ? 0ull : (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc1, src);
             Node t2;
             uint64_t pe2 = 0;
             if (valid) {
                 const Sub m = child(s1, k, select_bit(qb, j), d, pl);
                 t2 = apply(s1, m, pl);
-                pe2 = pe | ((uint64_t)m.enc << 16);
+                pe2 = Sink::kEnc ? pe | ((uint64_t)m.enc << 16) : 0ull;
             }
             const uint64_t f2 = memo_batch<kLogMemo2, true>(memo2, n_memo2, valid, t2, kTag2);
             uint32_t q3 = 0;

@@ -193,6 +193,7 @@ __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
 // block at a time (one atomic per block).  On pool exhaustion the job is `lost`
 // (re-run next round); its leaves already written stay valid candidates.
 struct KeySink {
+    static constexpr bool kEnc = false;    // keys only: the move encodings are dead
     uint4* keys;
     uint32_t* tags;
     unsigned long long* cursor;
@@ -238,7 +239,8 @@ struct KeySink {
 
 // One (row, roll) job.  KIND 0: non-doubles roll, 1: doubles roll, 2: either.
 // Returns 0 done, 1 LDS/HBM table overflow, 2 pool exhausted.
-// MK: revisit memo kind (-1 none, 0 separate depth-2/3 tables, 1 one combined table).
+// MK: revisit memo kind (-1 none, 0 separate depth-2/3 tables, 1 one combined table,
+// 2 tagged entries inside the dedup table itself).
 template <int LOG, typename SlotPtr, int MK, int KIND>
 __device__ __forceinline__ int enum_job(const S2& S, int job, SlotPtr tab, int cap_unique, uint4* memo,
                                         KeySink& sink, unsigned long long& leaves) {
@@ -252,11 +254,12 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, SlotPtr tab, int c
     for (int i = l; i < (1 << LOG); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = KIND == 1 || (KIND == 2 && r0 == r1);
     constexpr int kMemoN = MK == 1 ? (1 << kLogCMemo) : kMemoSlots;
-    if (MK >= 0 && dbl)
+    if ((MK == 0 || MK == 1) && dbl)
         for (int i = l; i < kMemoN; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     Gen<LOG, SlotPtr, KeySink, MK < 0 ? 0 : MK> g;
     g.tab = tab; g.pl = q; g.cap_unique = cap_unique; g.blocked = blocked;
+    if (MK == 2) memo = (uint4*)tab;    // non-null: pruning on (entries live in tab)
     g.memo2 = MK >= 0 && dbl ? memo : nullptr;
     g.memo3 = MK >= 0 && dbl ? (MK == 1 ? memo : memo + (1 << kLogMemo2)) : nullptr;
     g.sink = sink;
@@ -292,8 +295,8 @@ __device__ __forceinline__ KeySink make_sink(const S2& S) {
 
 // VARIANT 0: jobs (row, non-doubles roll) implicit, 1: (row, doubles roll)
 // implicit, 2: the explicit list.
-template <int LOG, int MK, int VARIANT>
-__global__ __launch_bounds__(64) void k_enum(S2 S) {
+template <int LOG, int MK, int VARIANT, int WPE = 1>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_enum(S2 S) {
     __shared__ uint4 tab[1 << LOG];
     __shared__ uint4 memo_[MK == 0 ? kMemoSlots : (MK == 1 ? (1 << kLogCMemo) : 1)];
     uint4* memo = MK >= 0 ? memo_ : nullptr;
@@ -869,14 +872,23 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
              retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>()};
         // doubles enumerator: dedup table 2^LOG slots + revisit memo kind (BGX_2PLY_HEAVY=LOG:MK)
-        int hlog = 9, hmk = 0;
-        if (const char* hv = getenv("BGX_2PLY_HEAVY")) { hlog = atoi(hv); const char* c = strchr(hv, ':'); if (c) hmk = atoi(c + 1); }
-        void (*kheavy)(S2) = k_enum<9, 0, 1>;
-        void (*klist)(S2) = k_enum<9, 0, 2>;
-        if (hlog == 8 && hmk == 0) { kheavy = k_enum<8, 0, 1>; klist = k_enum<8, 0, 2>; }
+        int hlog = 9, hmk = 2, hwpe = 0;
+        if (const char* hv = getenv("BGX_2PLY_HEAVY")) {
+            hlog = atoi(hv);
+            const char* c = strchr(hv, ':');
+            if (c) { hmk = atoi(c + 1); c = strchr(c + 1, ':'); if (c) hwpe = atoi(c + 1); }
+        }
+        void (*kheavy)(S2) = k_enum<9, 2, 1>;
+        void (*klist)(S2) = k_enum<9, 2, 2>;
+        if (hlog == 9 && hmk == 0) { kheavy = k_enum<9, 0, 1>; klist = k_enum<9, 0, 2>; }
+        else if (hlog == 9 && hmk == 2 && hwpe == 5) { kheavy = k_enum<9, 2, 1, 5>; klist = k_enum<9, 2, 2, 5>; }
+        else if (hlog == 9 && hmk == 2 && hwpe == 6) { kheavy = k_enum<9, 2, 1, 6>; klist = k_enum<9, 2, 2, 6>; }
+        else if (hlog == 8 && hmk == 2) { kheavy = k_enum<8, 2, 1>; klist = k_enum<8, 2, 2>; }
+        else if (hlog == 8 && hmk == 0) { kheavy = k_enum<8, 0, 1>; klist = k_enum<8, 0, 2>; }
         else if (hlog == 10 && hmk == 0) { kheavy = k_enum<10, 0, 1>; klist = k_enum<10, 0, 2>; }
         else if (hlog == 9 && hmk == 1) { kheavy = k_enum<9, 1, 1>; klist = k_enum<9, 1, 2>; }
-        else hlog = 9;
+        else if (hlog == 10 && hmk == 2) { kheavy = k_enum<10, 2, 1>; klist = k_enum<10, 2, 2>; }
+        else { hlog = 9; hmk = 2; }
         S.cap_heavy = (7 << hlog) / 8;
         if (const char* fs = getenv("BGX_2PLY_LDS_CAP")) {    // tests: force the overflow tiers ("first[:mid]")
             S.cap_light = S.cap_heavy = S.cap_mid = atoi(fs);

@@ -107,7 +107,7 @@ def test_two_ply_pool_retry_rounds(setup, monkeypatch):
 
 
 @pytest.mark.parametrize("caps", ["6:3584", "6"])
-@pytest.mark.parametrize("heavy", ["9:0", "10:0"])
+@pytest.mark.parametrize("heavy", ["9:2", "9:0", "10:0"])
 def test_two_ply_overflow_tiers(setup, monkeypatch, caps, heavy):
     """Every reply enumeration forced out of its first LDS table: into the
     4,096-slot LDS tier ("6:3584") or on through it to the HBM-table tier ("6").
