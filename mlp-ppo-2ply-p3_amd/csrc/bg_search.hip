@@ -242,15 +242,11 @@ struct KeySink {
 // MK: revisit memo kind (-1 none, 0 separate depth-2/3 tables, 1 one combined table,
 // 2 tagged entries inside the dedup table itself).
 template <int LOG, typename SlotPtr, int MK, int KIND>
-__device__ __forceinline__ int enum_job(const S2& S, int job, SlotPtr tab, int cap_unique, uint4* memo,
-                                        KeySink& sink, unsigned long long& leaves) {
-    const int row = job / 21, r = job - row * 21;
+__device__ __forceinline__ int enum_job(const S2& S, int job, int r, int q, const Node& sq, uint32_t blocked,
+                                        SlotPtr tab, int cap_unique, uint4* memo, KeySink& sink,
+                                        unsigned long long& leaves) {
     const int r0 = kRoll0[r], r1 = kRoll1[r];
     const int l = lane_id();
-    const int bv = (int)S.rowrec[(size_t)row * 64 + l];
-    const int q = rd(bv, 52);
-    uint32_t blocked;
-    const Node sq = node_from_bytes(bv, q, blocked);
     for (int i = l; i < (1 << LOG); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = KIND == 1 || (KIND == 2 && r0 == r1);
     constexpr int kMemoN = MK == 1 ? (1 << kLogCMemo) : kMemoSlots;
@@ -275,6 +271,23 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, SlotPtr tab, int c
     if (l == 0) S.maxlen[job] = (uint8_t)g.cur_max;
     leaves += (unsigned long long)(g.count ? g.count : 1);
     return 0;
+}
+
+// The replier's node of row `row` (its 64-byte record, one byte per lane).
+__device__ __forceinline__ Node row_node(int bv, int& q, uint32_t& blocked) {
+    q = rd(bv, 52);
+    return node_from_bytes(bv, q, blocked);
+}
+
+// job by its id alone (explicit lists, overflow tiers)
+template <int LOG, typename SlotPtr, int MK>
+__device__ __forceinline__ int enum_job_id(const S2& S, int job, SlotPtr tab, int cap_unique, uint4* memo,
+                                           KeySink& sink, unsigned long long& leaves) {
+    const int row = job / 21;
+    int q;
+    uint32_t blocked;
+    const Node sq = row_node((int)S.rowrec[(size_t)row * 64 + lane_id()], q, blocked);
+    return enum_job<LOG, SlotPtr, MK, 2>(S, job, job - row * 21, q, sq, blocked, tab, cap_unique, memo, sink, leaves);
 }
 
 __device__ __forceinline__ void queue_job(int32_t* count, int32_t* list, int cap, int job, int32_t* overflow_count,
@@ -302,19 +315,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     uint4* memo = MK >= 0 ? memo_ : nullptr;
     KeySink sink = make_sink(S);
     unsigned long long leaves = 0;
-    const int64_t n = VARIANT == 0 ? (int64_t)S.rows * 15 : VARIANT == 1 ? (int64_t)S.rows * 6 : *S.list_count;
-    for (int64_t i = blockIdx.x; i < n; i += gridDim.x) {
-        int job;
-        if (VARIANT == 0) { const int row = (int)(i / 15); job = row * 21 + kNdRoll[i - (int64_t)row * 15]; }
-        else if (VARIANT == 1) { const int row = (int)(i / 6); job = row * 21 + kDbRoll[i - (int64_t)row * 6]; }
-        else job = S.list[i];
-        const int st = enum_job<LOG, uint4*, MK, VARIANT>(S, job, tab, VARIANT == 0 ? S.cap_light : S.cap_heavy, memo,
-                                                             sink, leaves);
+    const int cap = VARIANT == 0 ? S.cap_light : S.cap_heavy;
+    auto done = [&](int st, int job) {
         if (st == 1) {
             const int qo = LOG < 10 ? 0 : 1;
             queue_job(S.qcount + qo, S.queues + (size_t)qo * kSlowQueue, kSlowQueue, job, S.retry_count, S.retry_list);
+        } else if (st == 2) {
+            queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
         }
-        else if (st == 2) queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
+    };
+    if (VARIANT == 2) {
+        const int n = *S.list_count;
+        for (int i = blockIdx.x; i < n; i += gridDim.x) {
+            const int job = S.list[i];
+            done(enum_job_id<LOG, uint4*, MK>(S, job, tab, cap, memo, sink, leaves), job);
+        }
+    } else {
+        // one row at a time: its 15 non-doubles (VARIANT 0) or 6 doubles rolls share
+        // the replier's node; the next row's record is loaded behind this row's work
+        int row = blockIdx.x;
+        int bv = row < S.rows ? (int)S.rowrec[(size_t)row * 64 + lane_id()] : 0;
+        for (; row < S.rows; row += gridDim.x) {
+            const int nrow = row + gridDim.x < S.rows ? row + gridDim.x : row;
+            const int bv_next = (int)S.rowrec[(size_t)nrow * 64 + lane_id()];
+            int q;
+            uint32_t blocked;
+            const Node sq = row_node(bv, q, blocked);
+            constexpr int nr = VARIANT == 0 ? 15 : 6;
+            #pragma unroll 1
+            for (int k = 0; k < nr; ++k) {
+                const int r = VARIANT == 0 ? kNdRoll[k] : kDbRoll[k];
+                const int job = row * 21 + r;
+                done(enum_job<LOG, uint4*, MK, VARIANT>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves), job);
+            }
+            bv = bv_next;
+        }
     }
     sink.finish();
     if (lane_id() == 0 && leaves) atomicAdd(S.leaves, leaves);
@@ -333,7 +368,7 @@ __global__ __launch_bounds__(64) void k_enum_tier(S2 S) {
     const int32_t* qin = S.queues + (size_t)QI * kSlowQueue;
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int job = qin[i];
-        const int st = enum_job<LOG, uint4*, 0, 2>(S, job, tab, min(S.cap_mid, cap_fast<LOG>()), memo,
+        const int st = enum_job_id<LOG, uint4*, 0>(S, job, tab, min(S.cap_mid, cap_fast<LOG>()), memo,
                                                    sink, leaves);
         if (st == 1) queue_job(S.qcount + QI + 1, S.queues + (size_t)(QI + 1) * kSlowQueue, kSlowQueue, job,
                                S.retry_count, S.retry_list);
@@ -352,7 +387,7 @@ __global__ __launch_bounds__(64) void k_enum_slow(S2 S, uint4* tables) {
     const int n = min(S.qcount[2], kSlowQueue);
     for (int i = blockIdx.x; i < n; i += gridDim.x) {
         const int job = S.queues[2 * (size_t)kSlowQueue + i];
-        const int st = enum_job<kLogSlotsSlow, uint4*, 0, 2>(S, job, tab, kCapSlow, memo, sink, leaves);
+        const int st = enum_job_id<kLogSlotsSlow, uint4*, 0>(S, job, tab, kCapSlow, memo, sink, leaves);
         if (st == 1 && lane_id() == 0) atomicOr(S.err, 1);
         else if (st == 2) queue_job(S.retry_count, S.retry_list, 0x7FFFFFFF, job, S.retry_count, S.retry_list);
     }
