@@ -144,7 +144,7 @@ def two_ply_bench(eng, batches: int, ws: int, dev):
     """C4: 2-ply expectimax over the 21 rolls for every lane's current position
     (B roots per GPU), value head MLP(198->40->1) on MFMA."""
     from bgx.policy import PolicyNet
-    from bgx.search import ValueHead, two_ply
+    from bgx.search import ValueHead, two_ply, two_ply_timings
     torch.manual_seed(1)
     vnet = PolicyNet(hidden_size=40).to(dev)
     vh = ValueHead(vnet)
@@ -153,22 +153,35 @@ def two_ply_bench(eng, batches: int, ws: int, dev):
     barrier(ws)
     t0 = time.perf_counter()
     leaves = jobs = 0
+    enum_ms = eval_ms = 0.0
     for _ in range(batches):
         _, _, _, st = two_ply(eng, vh)
         leaves += st["leaves"]
         jobs += st["jobs"]
+        te, tv = two_ply_timings(eng)
+        enum_ms += te
+        eval_ms += tv
     torch.cuda.synchronize(dev)
     barrier(ws)
     el = max_over_ranks(time.perf_counter() - t0, ws)
     roots = sum_over_ranks(float(eng.batch * batches), ws)
     leaves_all = sum_over_ranks(float(leaves), ws)
     flop_per_leaf = 2 * 198 * 40 + 2 * 40
+    # k_eval (the MFMA kernel): algorithmic FLOPs of its leaves / its HIP-event time
+    eval_tflops = leaves * flop_per_leaf / (eval_ms / batches * 1e-3) / batches / 1e12 if eval_ms > 0 else None
     return {"config": "C4: B=65536 roots/GPU, 2-ply expectimax over 21 rolls, value MLP 198->40->1 "
                       "(W1 split hi+lo on f16 MFMA, exact f16 features; fp32-equivalent)",
             "root_decisions_per_s": roots / el, "leaf_evals_per_s": leaves_all / el,
             "leaves_per_root": leaves_all / roots, "reply_enumerations": jobs * ws, "seconds": el,
-            "mfma_achieved_tflops": leaves_all * flop_per_leaf / el / 1e12,
-            "mfma_peak_tflops_f16_dense": 2500.0}
+            "enumeration_ms_per_batch": enum_ms / batches, "evaluation_ms_per_batch": eval_ms / batches,
+            "roofline": {"kernel": "k_eval: leaf pool -> f16-exact features -> W1 hi+lo on "
+                                   "v_mfma_f32_32x32x16_f16 -> value head -> per-job min (HIP events)",
+                         "bound": "mfma", "achieved": eval_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": eval_tflops / BF16_PEAK_TFLOPS if eval_tflops else None,
+                         "flop_per_leaf": flop_per_leaf,
+                         "issued_over_algorithmic": 2 * (64 / 40) * (208 / 198),
+                         "note": "issued MFMA work = algorithmic x 2 (W1 hi+lo split for fp32 accuracy) x 64/40 "
+                                 "(H=40 padded to two 32-row tiles) x 208/198 (K padding)"}}
 
 
 def main():

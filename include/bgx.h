@@ -176,6 +176,11 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float v
 int bgx_two_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float value_bias, int32_t* best_out,
                 float* bestq_out, float* q_out, uint64_t* stats_host, void* stream);
 
+/* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
+ * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
+ * evaluation (k_eval, the MFMA kernel). */
+int bgx_two_ply_timings(bgx_engine* e, float* ms2);
+
 /* Last HIP error string of this thread (diagnostics). */
 const char* bgx_last_error(void);
 

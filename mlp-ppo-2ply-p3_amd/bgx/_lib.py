@@ -43,6 +43,7 @@ SIGNATURES = {
     "bgx_value_pack": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P]),
     "bgx_one_ply": (ctypes.c_int, [_P, _P, _I32, ctypes.c_float, _P, _P, _P, _P]),
     "bgx_two_ply": (ctypes.c_int, [_P, _P, _I32, ctypes.c_float, _P, _P, _P, _P, _P]),
+    "bgx_two_ply_timings": (ctypes.c_int, [_P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
 }
 

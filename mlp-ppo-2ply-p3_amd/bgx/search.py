@@ -60,3 +60,12 @@ def two_ply(eng: Engine, vh: ValueHead, want_q: bool = False):
     check(L.bgx_two_ply(eng._h, _ptr(vh.packed), vh.hidden, vh.bias, _ptr(best), _ptr(bestq), _ptr(q),
                         ctypes.cast(stats, ctypes.c_void_p), _stream(dev)), "bgx_two_ply")
     return best, bestq, q, {"leaves": int(stats[0]), "jobs": int(stats[1]), "afterstates": int(stats[2])}
+
+
+def two_ply_timings(eng: Engine):
+    """(enumeration ms, evaluation ms) of the last two_ply call's first round,
+    timed with HIP events on the caller's stream."""
+    L = _lib.load()
+    ms = (ctypes.c_float * 2)()
+    check(L.bgx_two_ply_timings(eng._h, ctypes.cast(ms, ctypes.c_void_p)), "bgx_two_ply_timings")
+    return float(ms[0]), float(ms[1])

@@ -405,4 +405,7 @@ struct bgx_engine {
     size_t search_ws_bytes;
     void* search_pool;        // 2-ply leaf pool: keys [cap] x 16 B, then tags [cap] x 4 B
     size_t search_pool_cap;
+    hipStream_t search_side;  // 2-ply: second stream for the concurrent enumerator (created on demand)
+    hipEvent_t search_ev[5];  // 2-ply phase marks: start, enumerated, evaluated, fork, join
+    float search_ms[2];       // last bgx_two_ply call, round 0: enumeration ms, evaluation ms
 };

@@ -501,6 +501,8 @@ int bgx_engine_destroy(bgx_engine* e) {
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
                     e->slow_tables, e->search_ws, e->search_pool, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
+    for (hipEvent_t ev : e->search_ev) if (ev) (void)hipEventDestroy(ev);
+    if (e->search_side) (void)hipStreamDestroy(e->search_side);
     delete e;
     return BGX_OK;
 }

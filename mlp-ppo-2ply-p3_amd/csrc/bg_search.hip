@@ -965,23 +965,44 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         SCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device));
         SCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&g_eval, T == 1 ? k_eval<1> : k_eval<2>, 64 * kEvalWaves, 0));
         g_eval = (g_eval > 0 ? g_eval : 1) * (ncu > 0 ? ncu : 256);
+        if (!e->search_ev[0])
+            for (hipEvent_t& ev : e->search_ev) SCK(hipEventCreate(&ev));
+        const char* ov = getenv("BGX_2PLY_OVERLAP");    // "0": enumerators back to back (A/B)
+        const bool overlap = !(ov && ov[0] == '0');
+        if (overlap && !e->search_side) SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
+        SCK(hipEventRecord(e->search_ev[0], s));
         for (int round = 0;; ++round) {
             if (round == 0) {
-                hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
+                if (overlap) {       // the non-doubles enumerator beside the doubles one
+                    SCK(hipEventRecord(e->search_ev[3], s));
+                    SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
+                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, e->search_side, S);
+                    SCK(hipEventRecord(e->search_ev[4], e->search_side));
+                    SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
+                } else {
+                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
+                }
             } else {
                 hipLaunchKernelGGL(klist, dim3(g_list), dim3(64), 0, s, S);
             }
             hipLaunchKernelGGL((k_enum_tier<10, 0>), dim3(g_t0), dim3(64), 0, s, S);
             hipLaunchKernelGGL((k_enum_tier<kLogMid, 1>), dim3(g_mid), dim3(64), 0, s, S);
             hipLaunchKernelGGL(k_enum_slow, dim3(e->slow_waves), dim3(64), 0, s, S, e->slow_tables);
+            if (round == 0) SCK(hipEventRecord(e->search_ev[1], s));
             if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64 * kEvalWaves), 0, s, E);
             else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64 * kEvalWaves), 0, s, E);
             SCK(hipGetLastError());
+            if (round == 0) SCK(hipEventRecord(e->search_ev[2], s));
             Ctr hc;
             SCK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, s));
             SCK(hipStreamSynchronize(s));
             const int32_t nretry = hc.retry_count;
+            if (round == 0) {
+                SCK(hipEventElapsedTime(&e->search_ms[0], e->search_ev[0], e->search_ev[1]));
+                SCK(hipEventElapsedTime(&e->search_ms[1], e->search_ev[1], e->search_ev[2]));
+            }
             if (dbg)
                 fprintf(stderr, "[bgx 2-ply] round %d: pool %llu/%zu, tier1 %d, tier2 %d, retry %d, leaves %llu\n", round,
                         hc.cursor, pcap, hc.qcount[0] + hc.qcount[1], hc.qcount[2], hc.retry_count, hc.leaves);
@@ -1005,6 +1026,13 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         stats_host[1] = (uint64_t)jobs64;
         stats_host[2] = (uint64_t)rows64;
     }
+    return BGX_OK;
+}
+
+int bgx_two_ply_timings(bgx_engine* e, float* ms2) {
+    if (!e || !ms2) return BGX_EINVAL;
+    ms2[0] = e->search_ms[0];
+    ms2[1] = e->search_ms[1];
     return BGX_OK;
 }
 
