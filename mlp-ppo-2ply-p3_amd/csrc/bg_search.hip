@@ -46,6 +46,7 @@ constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
 constexpr uint32_t kTagNone = 0xFFFFFFFFu;
 constexpr int kLogLight = 8;       // non-doubles reply enumeration: 256-slot table (4 KiB)
 constexpr int kMaxRounds = 256;
+constexpr int kMaxChunks = 8;   // optional: rows in chunks, chunk i evaluated while chunk i+1 enumerates
 
 __constant__ float kOff15s[16] = {
     0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
@@ -166,7 +167,7 @@ __device__ __forceinline__ Node apply_move(Node s, uint64_t m, int pl) {
 // ------------------------------------------------------------------ 2-ply --
 struct S2 {
     const uint8_t* rowrec;            // [rows][64]: afterstate bytes 0..51, byte 52 = replier q
-    int32_t rows;
+    int32_t row0, row1;               // rows of this launch (implicit-job variants)
     uint4* keys;                      // leaf pool [cap]
     uint32_t* tags;                   // [cap] job | len << 29, kTagNone = unused slot
     unsigned long long* cursor;       // next free pool slot (kBlk granularity; may run past cap)
@@ -333,10 +334,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     } else {
         // one row at a time: its 15 non-doubles (VARIANT 0) or 6 doubles rolls share
         // the replier's node; the next row's record is loaded behind this row's work
-        int row = blockIdx.x;
-        int bv = row < S.rows ? (int)S.rowrec[(size_t)row * 64 + lane_id()] : 0;
-        for (; row < S.rows; row += gridDim.x) {
-            const int nrow = row + gridDim.x < S.rows ? row + gridDim.x : row;
+        int row = S.row0 + blockIdx.x;
+        int bv = row < S.row1 ? (int)S.rowrec[(size_t)row * 64 + lane_id()] : 0;
+        for (; row < S.row1; row += gridDim.x) {
+            const int nrow = row + gridDim.x < S.row1 ? row + gridDim.x : row;
             const int bv_next = (int)S.rowrec[(size_t)nrow * 64 + lane_id()];
             int q;
             uint32_t blocked;
@@ -441,7 +442,8 @@ struct Leaf {
 struct EvalArgs {
     const uint4* keys;
     const uint32_t* tags;
-    const unsigned long long* cursor;
+    const unsigned long long* lo;     // pool range [*lo, min(*hi, cap)) of this launch
+    const unsigned long long* hi;
     unsigned long long cap;
     const uint4* rowside;
     const uint8_t* maxlen;
@@ -541,10 +543,10 @@ __global__ __launch_bounds__(64 * kEvalWaves) void k_eval(EvalArgs E) {
     for (int i = threadIdx.x; i < kKB * T * 2 * 64; i += blockDim.x) wq[i] = E.w1q[i];
     for (int i = threadIdx.x; i < T * 16 * 64; i += blockDim.x) bw[i] = make_float2(E.b1p[i] * up, E.wvp[i]);
     __syncthreads();
-    const unsigned long long used = *E.cursor < E.cap ? *E.cursor : E.cap;
+    const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
     const unsigned long long tiles = used / 64;
     const unsigned long long stride = (unsigned long long)gridDim.x * kEvalWaves;
-    unsigned long long tile = (unsigned long long)blockIdx.x * kEvalWaves + (threadIdx.x >> 6);
+    unsigned long long tile = *E.lo / 64 + (unsigned long long)blockIdx.x * kEvalWaves + (threadIdx.x >> 6);
     if (tile >= tiles) return;
     LeafRaw raw[2];
     LeafRow row[2];
@@ -846,7 +848,13 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     Args& A = e->a;
     const size_t B = (size_t)A.B;
     // workspace head: [lane_off B i32][counters 256 B][overflow queues]
-    struct Ctr { int64_t rows; unsigned long long leaves, cursor; int32_t qcount[3], retry_count, list_count; };
+    struct Ctr {
+        int64_t rows;
+        unsigned long long leaves, cursor;
+        int32_t qcount[3], retry_count, list_count, pad;
+        unsigned long long snap[kMaxChunks + 1];      // pool cursor after each chunk's enumeration
+    };
+    static_assert(sizeof(Ctr) <= 256, "counters");
     const size_t o_ctr = align256(B * 4), o_q = o_ctr + 256, head = align256(o_q + (size_t)3 * kSlowQueue * 4);
     auto grow = [&](size_t need) -> int {
         if (e->search_ws_bytes >= need) return BGX_OK;
@@ -903,7 +911,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
                            lane_off, rows, rowrec, rowside);
         SCK(hipGetLastError());
-        S2 S{rowrec, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
+        S2 S{rowrec, 0, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
              retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>()};
         // doubles enumerator: dedup table 2^LOG slots + revisit memo kind (BGX_2PLY_HEAVY=LOG:MK)
@@ -933,7 +941,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const int T = value_tiles(hidden);
         const float* f16s = vpacked + sz_f32(T);
         const VNet vn = make_vnet(vpacked, hidden, value_bias);
-        EvalArgs E{nullptr, nullptr, &ctr->cursor, 0ull, rowside, maxlen, minv,
+        EvalArgs E{nullptr, nullptr, &ctr->snap[0], &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), vn.b1p, vn.wvp, (const int*)f16s, value_bias};
         const int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
         const int g_heavy = persistent_grid(e, kheavy, 32);
@@ -971,28 +979,64 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const bool overlap = !(ov && ov[0] == '0');
         if (overlap && !e->search_side) SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
         SCK(hipEventRecord(e->search_ev[0], s));
-        for (int round = 0;; ++round) {
-            if (round == 0) {
-                if (overlap) {       // the non-doubles enumerator beside the doubles one
-                    SCK(hipEventRecord(e->search_ev[3], s));
-                    SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
-                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, e->search_side, S);
-                    SCK(hipEventRecord(e->search_ev[4], e->search_side));
-                    SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
-                } else {
-                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
-                }
-            } else {
-                hipLaunchKernelGGL(klist, dim3(g_list), dim3(64), 0, s, S);
-            }
+        const char* cs = getenv("BGX_2PLY_CHUNKS");
+        int chunks = cs ? atoi(cs) : 1;     // measured: 2 / 4 / 8 chunks -8 / -12 / -17 % (the
+        // evaluator's LDS-heavy workgroups displace enumerator waves)
+        chunks = chunks < 1 ? 1 : (chunks > kMaxChunks ? kMaxChunks : chunks);
+        if (chunks > 1 && !e->search_eval) SCK(hipStreamCreateWithFlags(&e->search_eval, hipStreamNonBlocking));
+        auto eval = [&](hipStream_t st) {
+            if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
+            else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
+        };
+        auto tiers = [&]() {
             hipLaunchKernelGGL((k_enum_tier<10, 0>), dim3(g_t0), dim3(64), 0, s, S);
             hipLaunchKernelGGL((k_enum_tier<kLogMid, 1>), dim3(g_mid), dim3(64), 0, s, S);
             hipLaunchKernelGGL(k_enum_slow, dim3(e->slow_waves), dim3(64), 0, s, S, e->slow_tables);
-            if (round == 0) SCK(hipEventRecord(e->search_ev[1], s));
-            if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64 * kEvalWaves), 0, s, E);
-            else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64 * kEvalWaves), 0, s, E);
+        };
+        for (int round = 0;; ++round) {
+            if (round == 0) {
+                const int per = (rows + chunks - 1) / chunks;
+                for (int c = 0; c < chunks; ++c) {
+                    S.row0 = c * per < rows ? c * per : rows;
+                    S.row1 = S.row0 + per < rows ? S.row0 + per : rows;
+                    if (overlap) {       // the non-doubles enumerator beside the doubles one
+                        SCK(hipEventRecord(e->search_ev[3], s));
+                        SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
+                        hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                        hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, e->search_side, S);
+                        SCK(hipEventRecord(e->search_ev[4], e->search_side));
+                        SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
+                    } else {
+                        hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                        hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
+                    }
+                    tiers();
+                    if (chunks > 1) {
+                        // this chunk's pool range [snap[c], snap[c+1]) is complete: evaluate it on
+                        // the evaluation stream while the next chunk enumerates
+                        SCK(hipMemcpyAsync(&ctr->snap[c + 1], &ctr->cursor, 8, hipMemcpyDeviceToDevice, s));
+                        SCK(hipMemsetAsync(ctr->qcount, 0, 12, s));
+                        SCK(hipEventRecord(e->search_ev[3], s));
+                        SCK(hipStreamWaitEvent(e->search_eval, e->search_ev[3], 0));
+                        E.lo = &ctr->snap[c];
+                        E.hi = &ctr->snap[c + 1];
+                        eval(e->search_eval);
+                    }
+                }
+                SCK(hipEventRecord(e->search_ev[1], s));
+                if (chunks > 1) {
+                    SCK(hipEventRecord(e->search_ev[4], e->search_eval));
+                    SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
+                } else {
+                    eval(s);
+                }
+            } else {
+                hipLaunchKernelGGL(klist, dim3(g_list), dim3(64), 0, s, S);
+                tiers();
+                E.lo = &ctr->snap[0];
+                E.hi = &ctr->cursor;
+                eval(s);
+            }
             SCK(hipGetLastError());
             if (round == 0) SCK(hipEventRecord(e->search_ev[2], s));
             Ctr hc;
