@@ -59,8 +59,21 @@ for k in kernels:
                                "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch")})
         env["busy_ns_per_step"] += k["avg_ns"]
         env["hbm_bytes_per_step"] += k.get("hbm_bytes_per_launch") or 0.0
+# 2-ply evaluator (k_eval): MFMA busy cycles (SQ_VALU_MFMA_BUSY_CYCLES counts cycles,
+# 32 per v_mfma_f32_32x32x16; MI355X_MICROARCH.md constants table) over 1024 SIMDs x
+# the kernel's duration at 2.4 GHz, and its HBM read bytes (2 x FETCH_SIZE KiB)
+ev = {}
+mf = pmc("mfma", "SQ_VALU_MFMA_BUSY_CYCLES")
+ef = pmc("efetch", "FETCH_SIZE")
+ek = next((k for k in kernels if "k_eval" in k["name"]), None)
+if ek and mf:
+    busy = statistics.mean(next(iter(mf.values())))
+    ev = {"kernel": ek["name"], "avg_ns": ek["avg_ns"], "mfma_busy_cycles": busy,
+          "mfma_busy_frac_at_2p4GHz": busy / (1024 * ek["avg_ns"] * 2.4)}
+    if ef:
+        ev["hbm_read_bytes"] = 2 * statistics.mean(next(iter(ef.values()))) * 1024
 summary = {"command": "python bench.py " + cmd, "pmc_command": "python bench.py " + pmc_cmd,
-           "kernels": kernels[:20], "env_step": env}
+           "kernels": kernels[:20], "env_step": env, "two_ply_eval": ev}
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
 for k in kernels[:20]:
     print(f"{k['pct']:6.2f}% {k['avg_ns']/1e3:10.1f} us (tail {k.get('avg_ns_timed_tail', 0)/1e3:.1f}) "
