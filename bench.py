@@ -38,6 +38,8 @@ def parse():
                     help="also time full PPO iterations (T rollout steps + update); 0 = skip")
     ap.add_argument("--two-ply-batches", type=int, default=1,
                     help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
+    ap.add_argument("--c2-steps", type=int, default=50,
+                    help="C2: timed greedy 1-ply self-play steps at B=4096 (0 = skip)")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--shards", type=int, default=1,
                     help="the B games of a GPU as S engines of B/S lanes on S streams (measured: S=2 -4%%, "
@@ -138,6 +140,34 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 2):
             "env_steps_per_s_incl_update": steps / el, "seconds_per_iteration": el / iters,
             "rollout_s": sum(m["rollout_s"] for m in ms) / iters, "update_s": sum(m["update_s"] for m in ms) / iters,
             "losses_last": {k: ms[-1][k] for k in ("policy_loss", "value_loss", "entropy", "total_loss")}}
+
+
+def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev):
+    """C2: B games per GPU, greedy 1-ply self-play with the value head
+    MLP(198->40->1): every step = V over each lane's legal afterstates (mover's
+    one-hot, as legal_board_features) -> first argmax -> env.step."""
+    import bgx
+    from bgx.policy import PolicyNet
+    from bgx.search import ValueHead, one_ply
+    torch.manual_seed(2)
+    vh = ValueHead(PolicyNet(hidden_size=40).to(dev))
+    eng = bgx.Engine(batch=B, max_moves=500, seed=123 + rank, dice="philox", auto_reset=True, device=dev)
+    eng.reset(want_obs=False)
+    for _ in range(20):                                # burn-in + warm
+        best, _ = one_ply(eng, vh)
+        eng.step(best, want_obs=False, want_info=False)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        best, _ = one_ply(eng, vh)
+        eng.step(best, want_obs=False, want_info=False)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    el = max_over_ranks(time.perf_counter() - t0, ws)
+    return {"config": f"C2: B={B} games/GPU, 1-ply greedy self-play, value MLP 198->40->1 (argmax over afterstates)",
+            "env_steps_per_s": sum_over_ranks(float(B * steps), ws) / el, "ms_per_step": el * 1e3 / steps,
+            "steps": steps}
 
 
 def two_ply_bench(eng, batches: int, ws: int, dev):
@@ -343,6 +373,8 @@ def main():
                 a2, _, _ = net.act(net.rollout_inputs(eng2), seed=5, step=i)
                 eng2.step(a2, want_obs=False, want_info=False)
         line["two_ply"] = two_ply_bench(eng2, args.two_ply_batches, ws, dev)
+    if args.c2_steps > 0:
+        line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev)
     if args.horizon > 0 and args.workload in ("c3", "ppo"):
         line["ppo_iteration"] = ppo_iteration_bench(B, args.horizon, ws, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
