@@ -178,9 +178,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float v
 
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
- * evaluation after it (k_eval, the MFMA kernel).  With the optional chunked
- * pipeline (env BGX_2PLY_CHUNKS > 1; default 1) all but the last chunk's
- * evaluation overlaps the enumeration and ms2[1] is only its exposed tail. */
+ * evaluation after it (k_eval, the MFMA kernel). */
 int bgx_two_ply_timings(bgx_engine* e, float* ms2);
 
 /* Last HIP error string of this thread (diagnostics). */

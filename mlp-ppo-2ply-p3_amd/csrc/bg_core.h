@@ -406,15 +406,18 @@ struct Gen {
         BG_T0(tc);
         if (fill() + n >= cap_unique) { ovf = true; return; }
         fresh = place_batch<LOG_SLOTS, DEDUP>(tab, fresh, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+        BG_T1(13, tc);
+        BG_CNT(2, 1);
         if (DEDUP) n = __popcll(fresh);
         BG_CNT(8, n);
         n_unique += n;
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
+            BG_T0(ts);
             sink.push_lanes(fresh, t, enc, count, len);
+            BG_T1(11, ts);
             count += n;
         }
-        BG_T1(13, tc);
     }
 
     // Siblings (children of one node) are pairwise distinct afterstates
@@ -474,7 +477,9 @@ struct Gen {
                 const Sub m = child(s, k, select_bit(qb, j), d, pl);
                 leaf = apply(s, m, pl);
                 enc = Sink::kEnc ? pe | ((uint64_t)m.enc << shift) : 0ull;
+                BG_T0(tp);
                 found = probe_lane<LOG_SLOTS>(tab, (uint32_t)leaf.lo, (uint32_t)(leaf.lo >> 32), leaf.hi, leaf.k3, slot);
+                BG_T1(12, tp);
             }
             commit<true>(__ballot(valid && !found), leaf, enc, slot, len);
             if (ovf) return;
@@ -548,6 +553,7 @@ struct Gen {
             total += (uint32_t)__popcll(m) << b;
         }
         const uint64_t live = __ballot(cnt != 0u);
+        BG_CNT(15, total);
         for (uint32_t c = 0; c < total; c += 64) {
             const uint32_t pp = c + (uint32_t)l;
             const bool valid = pp < total;
@@ -596,6 +602,7 @@ struct Gen {
             total += (uint32_t)__popcll(m) << b;
         }
         const uint64_t live = __ballot(cnt != 0u);
+        BG_CNT(14, total);
         for (uint32_t c = 0; c < total; c += 64) {
             const uint32_t pp = c + (uint32_t)l;
             const bool valid = pp < total;
@@ -639,6 +646,7 @@ struct Gen {
     __device__ __forceinline__ void doubles_(const Node& s0, int d) {
         bool got4 = false;
         BG_CNT(0, 1);
+        BG_T0(t_phase_a);
         const Kids k1 = gen(s0, d, pl, blocked);
         Node t1;
         uint32_t e1 = 0;
@@ -663,7 +671,7 @@ struct Gen {
             uint32_t e2l = 0;
             const bool a2 = lane_child(s1, k2, d, t2, e2l);
             const uint64_t f2 = memo_batch<kLogMemo2>(memo2, n_memo2, a2, t2, kTag2);
-            BG_CNT(2, 1); BG_CNT(3, __popcll(f2)); BG_CNT(11, __popc(k2.bits));
+            BG_CNT(3, __popcll(f2));
             uint32_t q3 = 0;
             int x3 = -1;
             if ((f2 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; x3 = k.extra; }
@@ -681,16 +689,14 @@ struct Gen {
                     if (!got4) { insert(s2, m2, 2); if (ovf) return; }
                     continue;
                 }
-                BG_T0(tx);
                 Node t3;
                 uint32_t e3l = 0;
                 const bool a3 = lane_child(s2, k3, d, t3, e3l);
                 const uint64_t f3 = memo_batch<kLogMemo3>(memo3, n_memo3, a3, t3, kTag3);
-                BG_CNT(4, 1); BG_CNT(5, __popcll(f3)); BG_CNT(12, __popc(k3.bits));
+                BG_CNT(5, __popcll(f3));
                 uint32_t q4 = 0;
                 int x4 = -1;
                 if ((f3 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; x4 = k.extra; }
-                BG_T1(15, tx);
                 for (uint64_t b3 = f3; b3; b3 &= b3 - 1ull) {
                     const int i3 = __ffsll((unsigned long long)b3) - 1;
                     const uint32_t kb = rdl(q4, i3);
@@ -704,6 +710,7 @@ struct Gen {
                     // from the first node with children on, got4 holds: dead ends are
                     // no-ops and every remaining node's leaves go out as one flat batch
                     const uint64_t rest = b3 & __ballot(q4 != 0u);
+                    BG_T1(9, t_phase_a); BG_CNT(10, 1);
                     flat_leaves(rest, t3, q4, x4, m2 | ((uint64_t)e3l << 32), d, 48, 4);
                     if (ovf) return;
                     got4 = true;

@@ -406,7 +406,6 @@ struct bgx_engine {
     void* search_pool;        // 2-ply leaf pool: keys [cap] x 16 B, then tags [cap] x 4 B
     size_t search_pool_cap;
     hipStream_t search_side;  // 2-ply: second stream for the concurrent enumerator (created on demand)
-    hipStream_t search_eval;  // 2-ply: evaluation stream (chunked pipeline)
     hipEvent_t search_ev[5];  // 2-ply phase marks: start, enumerated, evaluated, fork, join
     float search_ms[2];       // last bgx_two_ply call, round 0: enumeration ms, evaluation ms
 };

@@ -503,7 +503,6 @@ int bgx_engine_destroy(bgx_engine* e) {
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (hipEvent_t ev : e->search_ev) if (ev) (void)hipEventDestroy(ev);
     if (e->search_side) (void)hipStreamDestroy(e->search_side);
-    if (e->search_eval) (void)hipStreamDestroy(e->search_eval);
     delete e;
     return BGX_OK;
 }

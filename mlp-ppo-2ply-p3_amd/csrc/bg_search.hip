@@ -46,7 +46,6 @@ constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
 constexpr uint32_t kTagNone = 0xFFFFFFFFu;
 constexpr int kLogLight = 8;       // non-doubles reply enumeration: 256-slot table (4 KiB)
 constexpr int kMaxRounds = 256;
-constexpr int kMaxChunks = 8;   // optional: rows in chunks, chunk i evaluated while chunk i+1 enumerates
 
 __constant__ float kOff15s[16] = {
     0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
@@ -852,7 +851,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         int64_t rows;
         unsigned long long leaves, cursor;
         int32_t qcount[3], retry_count, list_count, pad;
-        unsigned long long snap[kMaxChunks + 1];      // pool cursor after each chunk's enumeration
+        unsigned long long zero;                      // start of the evaluated pool range
     };
     static_assert(sizeof(Ctr) <= 256, "counters");
     const size_t o_ctr = align256(B * 4), o_q = o_ctr + 256, head = align256(o_q + (size_t)3 * kSlowQueue * 4);
@@ -941,7 +940,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const int T = value_tiles(hidden);
         const float* f16s = vpacked + sz_f32(T);
         const VNet vn = make_vnet(vpacked, hidden, value_bias);
-        EvalArgs E{nullptr, nullptr, &ctr->snap[0], &ctr->cursor, 0ull, rowside, maxlen, minv,
+        EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), vn.b1p, vn.wvp, (const int*)f16s, value_bias};
         const int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
         const int g_heavy = persistent_grid(e, kheavy, 32);
@@ -963,7 +962,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             SCK(hipMalloc(&e->search_pool, cap * 20));
             e->search_pool_cap = cap;
         }
-        const size_t pcap = e->search_pool_cap;
+        const size_t pcap = cap;           // the pool may be larger (kept from a bigger call)
         S.keys = (uint4*)e->search_pool;
         S.tags = (uint32_t*)(S.keys + pcap);
         E.keys = S.keys;
@@ -979,62 +978,40 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const bool overlap = !(ov && ov[0] == '0');
         if (overlap && !e->search_side) SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
         SCK(hipEventRecord(e->search_ev[0], s));
-        const char* cs = getenv("BGX_2PLY_CHUNKS");
-        int chunks = cs ? atoi(cs) : 1;     // measured: 2 / 4 / 8 chunks -8 / -12 / -17 % (the
-        // evaluator's LDS-heavy workgroups displace enumerator waves)
-        chunks = chunks < 1 ? 1 : (chunks > kMaxChunks ? kMaxChunks : chunks);
-        if (chunks > 1 && !e->search_eval) SCK(hipStreamCreateWithFlags(&e->search_eval, hipStreamNonBlocking));
         auto eval = [&](hipStream_t st) {
             if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
             else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
         };
+        // retry rounds run few waves: every wave holding a block wastes its unused
+        // part, and a round must leave pool for its jobs to finish (progress with any pool)
+        int gcap = 1 << 30;
+        auto g = [&](int grid) { return grid < gcap ? grid : gcap; };
         auto tiers = [&]() {
-            hipLaunchKernelGGL((k_enum_tier<10, 0>), dim3(g_t0), dim3(64), 0, s, S);
-            hipLaunchKernelGGL((k_enum_tier<kLogMid, 1>), dim3(g_mid), dim3(64), 0, s, S);
-            hipLaunchKernelGGL(k_enum_slow, dim3(e->slow_waves), dim3(64), 0, s, S, e->slow_tables);
+            hipLaunchKernelGGL((k_enum_tier<10, 0>), dim3(g(g_t0)), dim3(64), 0, s, S);
+            hipLaunchKernelGGL((k_enum_tier<kLogMid, 1>), dim3(g(g_mid)), dim3(64), 0, s, S);
+            hipLaunchKernelGGL(k_enum_slow, dim3(g(e->slow_waves)), dim3(64), 0, s, S, e->slow_tables);
         };
         for (int round = 0;; ++round) {
             if (round == 0) {
-                const int per = (rows + chunks - 1) / chunks;
-                for (int c = 0; c < chunks; ++c) {
-                    S.row0 = c * per < rows ? c * per : rows;
-                    S.row1 = S.row0 + per < rows ? S.row0 + per : rows;
-                    if (overlap) {       // the non-doubles enumerator beside the doubles one
-                        SCK(hipEventRecord(e->search_ev[3], s));
-                        SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
-                        hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                        hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, e->search_side, S);
-                        SCK(hipEventRecord(e->search_ev[4], e->search_side));
-                        SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
-                    } else {
-                        hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                        hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
-                    }
-                    tiers();
-                    if (chunks > 1) {
-                        // this chunk's pool range [snap[c], snap[c+1]) is complete: evaluate it on
-                        // the evaluation stream while the next chunk enumerates
-                        SCK(hipMemcpyAsync(&ctr->snap[c + 1], &ctr->cursor, 8, hipMemcpyDeviceToDevice, s));
-                        SCK(hipMemsetAsync(ctr->qcount, 0, 12, s));
-                        SCK(hipEventRecord(e->search_ev[3], s));
-                        SCK(hipStreamWaitEvent(e->search_eval, e->search_ev[3], 0));
-                        E.lo = &ctr->snap[c];
-                        E.hi = &ctr->snap[c + 1];
-                        eval(e->search_eval);
-                    }
-                }
-                SCK(hipEventRecord(e->search_ev[1], s));
-                if (chunks > 1) {
-                    SCK(hipEventRecord(e->search_ev[4], e->search_eval));
+                if (overlap) {       // the non-doubles enumerator beside the doubles one
+                    SCK(hipEventRecord(e->search_ev[3], s));
+                    SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
+                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, e->search_side, S);
+                    SCK(hipEventRecord(e->search_ev[4], e->search_side));
                     SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
                 } else {
-                    eval(s);
+                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
                 }
-            } else {
-                hipLaunchKernelGGL(klist, dim3(g_list), dim3(64), 0, s, S);
                 tiers();
-                E.lo = &ctr->snap[0];
-                E.hi = &ctr->cursor;
+                SCK(hipEventRecord(e->search_ev[1], s));
+                eval(s);
+            } else {
+                const long long blocks = (long long)(pcap / kBlk);
+                gcap = (int)(blocks / 16 > 1 ? (blocks / 16 < (1 << 30) ? blocks / 16 : (1 << 30)) : 1);
+                hipLaunchKernelGGL(klist, dim3(g(g_list)), dim3(64), 0, s, S);
+                tiers();
                 eval(s);
             }
             SCK(hipGetLastError());

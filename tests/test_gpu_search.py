@@ -99,7 +99,7 @@ def test_two_ply_pool_retry_rounds(setup, monkeypatch):
     bgx, net, vh, eng = setup
     from bgx.search import two_ply
     best, bestq, q, st = two_ply(eng, vh, want_q=True)
-    monkeypatch.setenv("BGX_2PLY_POOL", "32768")
+    monkeypatch.setenv("BGX_2PLY_POOL", "65536")
     best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
     assert st2["leaves"] == st["leaves"]
     assert torch.equal(torch.nan_to_num(q2, 7.0), torch.nan_to_num(q, 7.0))
