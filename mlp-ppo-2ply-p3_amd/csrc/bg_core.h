@@ -234,18 +234,32 @@ __device__ __forceinline__ bool probe_lane(SlotPtr tab, uint32_t a, uint32_t b, 
 // sequence, and competes in the next round.  Returns `fresh` minus duplicates;
 // the kept lane of equal keys is the lowest (equal keys share their probe
 // chain, so they always meet on the same slot).  Linear probing stays valid.
+// LDS tables (LOG_SLOTS <= 12) elect the winners with one ds_max_u32 of
+// (64 - lane) on the target slot's last word and a read-back (3 LDS operations
+// per round); the HBM tier compares slots lane by lane (v_readlane loop).
 template <int LOG_SLOTS, bool DEDUP, typename SlotPtr>
 __device__ __forceinline__ uint64_t place_batch(SlotPtr tab, uint64_t fresh, uint32_t a, uint32_t b, uint32_t c,
                                                 uint32_t d, uint32_t slot) {
     constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
+    constexpr bool kLds = LOG_SLOTS <= 12;
     const int lane = threadIdx.x & 63;
     uint64_t pend = fresh;
     while (pend) {
         bool win = (pend >> lane) & 1ull;
-        for (uint64_t m = pend; m; m &= m - 1ull) {
-            const int src = __ffsll((unsigned long long)m) - 1;
-            const uint32_t hs = rdl(slot, src);
-            win = win && !(src < lane && slot == hs);
+        if (kLds) {
+            // the claim marks are transient: every claimed slot is empty and is
+            // overwritten by its winner's key before any lane reads the table again
+            const uint32_t mark = 64u - (uint32_t)lane;
+            uint32_t* w = (uint32_t*)&tab[slot] + 3;
+            if (win) atomicMax(w, mark);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            if (win) win = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) == mark;
+        } else {
+            for (uint64_t m = pend; m; m &= m - 1ull) {
+                const int src = __ffsll((unsigned long long)m) - 1;
+                const uint32_t hs = rdl(slot, src);
+                win = win && !(src < lane && slot == hs);
+            }
         }
         if (win) tab[slot] = make_uint4(a, b, c, d);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
