@@ -281,6 +281,19 @@ __device__ __forceinline__ uint64_t place_batch(SlotPtr tab, uint64_t fresh, uin
     return fresh;
 }
 
+// The lane whose run [pre, pre + cnt) holds flat position pp: the first lane with
+// inclusive prefix incl = pre + cnt > pp (incl is non-decreasing over the lanes,
+// so it is a lane with cnt > 0).  Binary search, 6 ds_bpermute.
+__device__ __forceinline__ int parent_of(uint32_t pp, uint32_t incl) {
+    int i = 0;
+    #pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)incl, i + st - 1);
+        i = v <= pp ? i + st : i;
+    }
+    return i < 64 ? i : 63;
+}
+
 __device__ __forceinline__ int lane_rank(uint64_t m) {          // set bits of m below this lane
     const int lane = threadIdx.x & 63;
     return __popcll(m & ((1ull << lane) - 1ull));
@@ -464,19 +477,12 @@ struct Gen {
             pre += (uint32_t)__popcll(m & below) << b;
             total += (uint32_t)__popcll(m) << b;
         }
-        const uint64_t live = __ballot(cnt != 0u);
         BG_CNT(6, 1);
         BG_CNT(7, total);
         for (uint32_t c = 0; c < total; c += 64) {
             const uint32_t pp = c + (uint32_t)l;
             const bool valid = pp < total;
-            int src = 0;
-            for (uint64_t m = live; m; m &= m - 1ull) {
-                const int i = __ffsll((unsigned long long)m) - 1;
-                const uint32_t pi = rdl(pre, i);
-                if (pi >= c + 64u) break;
-                src = pp >= pi ? i : src;
-            }
+            const int src = parent_of(pp, pre + cnt);
             const uint32_t qb = (uint32_t)__shfl((int)q, src);
             const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
             const Node s = shfl_node(t, src);
@@ -566,18 +572,11 @@ struct Gen {
             pre += (uint32_t)__popcll(m & below) << b;
             total += (uint32_t)__popcll(m) << b;
         }
-        const uint64_t live = __ballot(cnt != 0u);
         BG_CNT(15, total);
         for (uint32_t c = 0; c < total; c += 64) {
             const uint32_t pp = c + (uint32_t)l;
             const bool valid = pp < total;
-            int src = 0;
-            for (uint64_t m = live; m; m &= m - 1ull) {
-                const int i = __ffsll((unsigned long long)m) - 1;
-                const uint32_t pi = rdl(pre, i);
-                if (pi >= c + 64u) break;
-                src = pp >= pi ? i : src;
-            }
+            const int src = parent_of(pp, pre + cnt);
             const uint32_t qb = (uint32_t)__shfl((int)q3, src);
             const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
             const Node s2 = shfl_node(t2, src);
@@ -615,18 +614,11 @@ struct Gen {
             pre += (uint32_t)__popcll(m & below) << b;
             total += (uint32_t)__popcll(m) << b;
         }
-        const uint64_t live = __ballot(cnt != 0u);
         BG_CNT(14, total);
         for (uint32_t c = 0; c < total; c += 64) {
             const uint32_t pp = c + (uint32_t)l;
             const bool valid = pp < total;
-            int src = 0;
-            for (uint64_t m = live; m; m &= m - 1ull) {
-                const int i = __ffsll((unsigned long long)m) - 1;
-                const uint32_t pi = rdl(pre, i);
-                if (pi >= c + 64u) break;
-                src = pp >= pi ? i : src;
-            }
+            const int src = parent_of(pp, pre + cnt);
             const uint32_t qb = (uint32_t)__shfl((int)q2, src);
             const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
             const Node s1 = shfl_node(t1, src);
