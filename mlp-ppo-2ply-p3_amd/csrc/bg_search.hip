@@ -63,28 +63,39 @@ __device__ __forceinline__ int hid(int r, int h) { return (r & 3) + 8 * (r >> 2)
 // Value net packed for MFMA (bgx_value_pack), in floats:
 //   f32 section (1-ply):  w1p [99][T][64], b1p [T][16][64], wvp [T][16][64]
 //                         (= value_head.weight[32t + hid(r, l>>5)]), bv, 3 pad
-//   f16 section (2-ply):  hdr [4] (e1 as int bits), w1q [13][T][2][64] x uint4:
-//                         lane l, part 0 = hi / 1 = lo of W1s[32t + (l&31)][kperm(kb, l>>5, i)],
-//                         i = 0..7, W1s = W1 * 2^e1 with the two `off` columns divided by 15
-//                         (the features are then exact small integers / halves in f16).
+//   f16 section (2-ply):  hdr [4] (e1 as int bits), then NT = ceil(H/16) tiles of
+//                         16 hidden units with their hi AND lo parts in one 32-row
+//                         MFMA tile (row m: unit 16t + (m&7) + 8(m>>4), part (m>>3)&1):
+//     w1q [13][NT][64] x uint4   lane l: the 8 f16 of row l&31 at k = kperm(kb, l>>5, i),
+//                                i = 0..7, of W1s = [W1 | b1] * 2^e1 (the two `off`
+//                                columns divided by 15; b1 rides a constant-1 feature)
+//     wvq [NT][8][64] f32        value_head.weight[unit(t, j, l)] * 2^-e1 for the
+//                                accumulator pair (r, r+4), r = j < 4 ? j : j + 4
+// The features are then exact small integers / halves in f16, so one hi and one
+// lo MFMA product give fp32-grade accuracy, and hi + lo of a unit are summed
+// from two accumulator registers of the same lane.
 struct VNet { const float* w1p; const float* b1p; const float* wvp; float bv; };
 
 __host__ __device__ inline int sz_f32(int T) { return kK1 * T * 64 + 2 * T * 16 * 64 + 4; }
-__host__ __device__ inline int sz_f16(int T) { return 4 + kKB * T * 2 * 64 * 4; }
+__host__ __device__ inline int sz_f16(int NT) { return 4 + kKB * NT * 64 * 4 + NT * 8 * 64; }
 
-// Permuted K order of the f16 section: k-blocks 0-5 = P1 points, 6-11 = P2 points
-// (lane half h of block kb holds points 2pp, 2pp+1 with pp = 2(kb%6) + h, four
-// units each), block 12 = [bar1, off1, bar2, off2, onehot0, onehot1] on h = 0.
-// Returns the reference feature index (immutable_board.py:171-212) or -1 (pad).
+constexpr int kFeatBias = -2;
+// Permuted K order of the f16 section: k-blocks 0-5 = P1 points, 6-11 = P2 points;
+// lane half h of block kb holds points 2pp, 2pp+1 with pp = 2(kb%6) + h, as
+// [u0(a), u0(b), u1(a), u1(b), u2(a), u2(b), u3(a), u3(b)] (point pairs packed for
+// u16x2 arithmetic); block 12 = [bar1, off1, bar2, off2, onehot0, onehot1, 1 (bias), 0]
+// on h = 0.  Returns the reference feature index (immutable_board.py:171-212),
+// kFeatBias or -1 (pad).
 __host__ __device__ inline int kperm(int kb, int h, int i) {
     if (kb < 12) {
-        const int P = kb / 6, pp = 2 * (kb % 6) + h, point = 2 * pp + (i >> 2);
-        return 98 * P + 4 * point + (i & 3);
+        const int P = kb / 6, pp = 2 * (kb % 6) + h, point = 2 * pp + (i & 1);
+        return 98 * P + 4 * point + (i >> 1);
     }
     if (h) return -1;
-    const int ex[8] = {96, 97, 194, 195, 196, 197, -1, -1};
+    const int ex[8] = {96, 97, 194, 195, 196, 197, kFeatBias, -1};
     return ex[i];
 }
+
 // Feature k of the board (root bytes `ab` in LDS) after player q moved to the
 // afterstate with key (klo, khi, k3): q's counts come from the key nibbles, the
 // other side's from ab minus the hit blots; one-hot = `cur`.
@@ -448,9 +459,7 @@ struct EvalArgs {
     const uint8_t* maxlen;
     int32_t* minv;                    // [jobs] ordered-int encoding of the min
     const uint4* w1q;
-    const float* b1p;
-    const float* wvp;
-    const int* hdr;
+    const float* wvq;
     float bv;
 };
 
@@ -488,30 +497,44 @@ __device__ __forceinline__ Leaf make_leaf(const LeafRaw& r, const LeafRow& w) {
     return L;
 }
 
-__device__ __forceinline__ uint32_t h16(float x) {
-    return (uint32_t)__builtin_bit_cast(uint16_t, (_Float16)x);
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+
+// (a, b) small non-negative integers (< 1024) -> the f16 pair (a*s0, b*s1) exactly:
+// 1024 + k is an f16 with unit spacing, so (bits(k) | 0x6400) - 1024 == k.
+__device__ __forceinline__ uint32_t f16_pair(uint32_t ab, float s0, float s1) {
+    const h16x2 t = __builtin_bit_cast(h16x2, ab | 0x64006400u);
+    const h16x2 sc = {(_Float16)s0, (_Float16)s1};
+    const h16x2 r = t * sc - (h16x2){(_Float16)(1024.0f * s0), (_Float16)(1024.0f * s1)};
+    return __builtin_bit_cast(uint32_t, r);
 }
 
-// the four units of a point with n checkers (immutable_board.py:180-195) as f16 pairs
-__device__ __forceinline__ uint2 units16(uint32_t n) {
-    const uint32_t a = (n >= 1u ? 0x3C00u : 0u) | (n >= 2u ? 0x3C000000u : 0u);
-    const uint32_t c = n >= 3u ? (0x3C00u | (h16((float)((int)n - 3) * 0.5f) << 16)) : 0u;
-    return make_uint2(a, c);
+// the four units of two points with counts (a, b) (immutable_board.py:180-195) as
+// f16 pairs [u_k(a), u_k(b)], k = 0..3: n>=1, n>=2, n>=3, (n-3)/2 if n>=3
+__device__ __forceinline__ uint4 units_pair(uint32_t byte) {
+    const u16x2 x = __builtin_bit_cast(u16x2, (byte & 15u) | ((byte & 0xF0u) << 12));
+    const u16x2 one = {1, 1}, two = {2, 2}, three = {3, 3}, f1 = {0x3C00, 0x3C00};
+    const u16x2 u0 = __builtin_elementwise_min(x, one) * f1;
+    const u16x2 u1 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(x, one), one) * f1;
+    const u16x2 u2 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(x, two), one) * f1;
+    const uint32_t u3 = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, three));
+    return make_uint4(__builtin_bit_cast(uint32_t, u0), __builtin_bit_cast(uint32_t, u1),
+                      __builtin_bit_cast(uint32_t, u2), f16_pair(u3, 0.5f, 0.5f));
 }
 
 // B operand of k-block kb for this lane's half h (permuted K order, kperm)
 __device__ __forceinline__ f16x8 feat16(const Leaf& L, int kb, int h) {
     uint4 v;
     if (kb < 12) {
-        const int P = kb / 6, pp = 2 * (kb % 6) + h;
-        const uint32_t byte = kb % 6 < 4 ? (uint32_t)(L.lo[P] >> (8 * pp)) & 0xFFu
-                                         : (L.hi[P] >> (8 * (pp - 8))) & 0xFFu;
-        const uint2 u0 = units16(byte & 15u), u1 = units16(byte >> 4);
-        v = make_uint4(u0.x, u0.y, u1.x, u1.y);
+        const int P = kb / 6, k6 = kb % 6;
+        // points 4 k6 + 2h, +1: byte (2 k6 + h) of the 96-bit nibble vector
+        const uint32_t dw = k6 < 2 ? (uint32_t)L.lo[P] : (k6 < 4 ? (uint32_t)(L.lo[P] >> 32) : L.hi[P]);
+        const uint32_t byte = (dw >> (16 * (k6 & 1) + 8 * h)) & 0xFFu;
+        v = units_pair(byte);
     } else if (h == 0) {
-        v = make_uint4(h16((float)L.bar[0] * 0.5f) | (h16((float)L.off[0]) << 16),
-                       h16((float)L.bar[1] * 0.5f) | (h16((float)L.off[1]) << 16),
-                       L.q == 0 ? 0x3C00u : 0x3C000000u, 0u);
+        v = make_uint4(f16_pair(L.bar[0] | (L.off[0] << 16), 0.5f, 1.0f),
+                       f16_pair(L.bar[1] | (L.off[1] << 16), 0.5f, 1.0f),
+                       L.q == 0 ? 0x3C00u : 0x3C000000u, 0x3C00u);
     } else {
         v = make_uint4(0u, 0u, 0u, 0u);
     }
@@ -525,22 +548,22 @@ __device__ __forceinline__ int ord_f32(float v) {
 __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
 
 // Pool tiles of 64 leaves (two 32-column MFMA tiles sharing the weight
-// fragments): X1s = W1s . F^T + b1 2^e1 on v_mfma_f32_32x32x16_f16 (hi and lo
-// parts of W1s, features exact), V = wv . relu(X1s 2^-e1) + bv, then per job the
-// min over its leaves (leaves of a job are contiguous in the pool).
-// Workgroup = 4 waves sharing the packed weights in LDS (T = 2: 53 KiB of W1
-// fragments + 16 KiB of bias / value-head lanes); every wave walks its own tiles
-// with the next tile's pool entries in flight during the current tile's MFMAs.
+// fragments): X1s = [W1 | b1]s . [F | 1]^T on v_mfma_f32_32x32x16_f16, one MFMA per
+// (k-block, 16 hidden units, 32 leaves) -- the units' hi and lo weight parts sit in
+// rows m and m+8 of the same tile (accumulator registers r and r+4 of a lane) --
+// then V = sum wv 2^-e1 relu(hi + lo) + bv, and per job the min over its leaves
+// (leaves of a job are contiguous in the pool): segmented min over each 32-column
+// tile, one atomicMin per job segment.  Workgroup = 4 waves sharing the packed
+// weights in LDS (NT = 3 for H = 40: 39 KiB); every wave walks its own tiles with
+// the next tile's pool entries in flight during the current tile's MFMAs.
 constexpr int kEvalWaves = 4;
-template <int T>
+template <int NT>
 __global__ __launch_bounds__(64 * kEvalWaves) void k_eval(EvalArgs E) {
-    __shared__ uint4 wq[kKB * T * 2 * 64];
-    __shared__ float2 bw[T * 16 * 64];
+    __shared__ uint4 wq[kKB * NT * 64];
+    __shared__ float wvs[NT * 8 * 64];
     const int l = lane_id(), h = l >> 5, c = l & 31;
-    const int e1 = E.hdr[0];
-    const float up = ldexpf(1.0f, e1), down = ldexpf(1.0f, -e1);
-    for (int i = threadIdx.x; i < kKB * T * 2 * 64; i += blockDim.x) wq[i] = E.w1q[i];
-    for (int i = threadIdx.x; i < T * 16 * 64; i += blockDim.x) bw[i] = make_float2(E.b1p[i] * up, E.wvp[i]);
+    for (int i = threadIdx.x; i < kKB * NT * 64; i += blockDim.x) wq[i] = E.w1q[i];
+    for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = E.wvq[i];
     __syncthreads();
     const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
     const unsigned long long tiles = used / 64;
@@ -556,32 +579,23 @@ __global__ __launch_bounds__(64 * kEvalWaves) void k_eval(EvalArgs E) {
         #pragma unroll
         for (int n = 0; n < 2; ++n) L[n] = make_leaf(raw[n], row[n]);
         // an opaque zero offset per tile keeps the LDS fragment reads inside the loop
-        // (hoisted, the 52 fragments would take 208 registers: one wave per SIMD)
+        // (hoisted, the 39 fragments would take 156 registers)
         int z = 0;
         __asm__ volatile("" : "+s"(z));
         const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
         #pragma unroll
         for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
-        f32x16 x[2][T];
-        #pragma unroll
-        for (int t = 0; t < T; ++t)
-            #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float b = bw[(t * 16 + r) * 64 + l + z].x;
-                x[0][t][r] = b;
-                x[1][t][r] = b;
-            }
+        f32x16 x[2][NT];
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) {
             const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
             #pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * T + t) * 2 + 0) * 64 + l + z]);
-                const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * T + t) * 2 + 1) * 64 + l + z]);
-                x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f0, x[0][t], 0, 0, 0);
-                x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f1, x[1][t], 0, 0, 0);
-                x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, x[0][t], 0, 0, 0);
-                x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f1, x[1][t], 0, 0, 0);
+            for (int t = 0; t < NT; ++t) {
+                const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + t) * 64 + l + z]);
+                const f32x16 c0 = kb == 0 ? (f32x16){} : x[0][t];
+                const f32x16 c1 = kb == 0 ? (f32x16){} : x[1][t];
+                x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, c0, 0, 0, 0);
+                x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, c1, 0, 0, 0);
             }
         }
         #pragma unroll
@@ -590,10 +604,12 @@ __global__ __launch_bounds__(64 * kEvalWaves) void k_eval(EvalArgs E) {
         for (int n = 0; n < 2; ++n) {
             float v = 0.0f;
             #pragma unroll
-            for (int t = 0; t < T; ++t)
+            for (int t = 0; t < NT; ++t)
                 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    v = fmaf(fmaxf(x[n][t][r] * down, 0.0f), bw[(t * 16 + r) * 64 + l + z].y, v);
+                for (int j = 0; j < 8; ++j) {
+                    const int r = j < 4 ? j : j + 4;
+                    v = fmaf(fmaxf(x[n][t][r] + x[n][t][r + 4], 0.0f), wvs[(t * 8 + j) * 64 + l + z], v);
+                }
             v += __shfl_xor(v, 32);
             v += E.bv;
             const int jb = L[n].job;
@@ -637,14 +653,16 @@ __device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
     lo = (_Float16)(x - (float)hi);
 }
 
-// f16 section of the value pack (one workgroup): e1 from max |W1s|, then w1q.
-__global__ __launch_bounds__(1024) void k_value_pack16(const float* W1, int H, int T, int* hdr, _Float16* w1q) {
+// f16 section of the value pack (one workgroup): e1 from max |[W1s | b1]|, then
+// w1q and wvq (layout above).
+__global__ __launch_bounds__(1024) void k_value_pack16(const float* W1, const float* b1, const float* wv, int H,
+                                                       int NT, int* hdr, _Float16* w1q, float* wvq) {
     __shared__ float red[1024];
     const int tid = threadIdx.x;
     float mx = 0.0f;
-    for (int i = tid; i < H * 198; i += 1024) {
-        const int f = i % 198;
-        const float w = (f == 97 || f == 195) ? W1[i] / 15.0f : W1[i];
+    for (int i = tid; i < H * 199; i += 1024) {
+        const int u = i / 199, f = i % 199;
+        const float w = f == 198 ? b1[u] : ((f == 97 || f == 195) ? W1[u * 198 + f] / 15.0f : W1[u * 198 + f]);
         mx = fmaxf(mx, fabsf(w));
     }
     red[tid] = mx;
@@ -661,21 +679,24 @@ __global__ __launch_bounds__(1024) void k_value_pack16(const float* W1, int H, i
         e1 = e1 < -100 ? -100 : (e1 > 100 ? 100 : e1);
     }
     if (tid == 0) { hdr[0] = e1; hdr[1] = 0; hdr[2] = 0; hdr[3] = 0; }
-    const int n = kKB * T * 64 * 8;
+    const int n = kKB * NT * 64 * 8;
     for (int idx = tid; idx < n; idx += 1024) {
-        const int i = idx & 7, l = (idx >> 3) & 63, t = (idx >> 9) % T, kb = (idx >> 9) / T;
-        const int m = 32 * t + (l & 31);
+        const int i = idx & 7, l = (idx >> 3) & 63, t = (idx >> 9) % NT, kb = (idx >> 9) / NT;
+        const int m = l & 31, unit = 16 * t + (m & 7) + 8 * (m >> 4), part = (m >> 3) & 1;
         const int f = kperm(kb, l >> 5, i);
         float w = 0.0f;
-        if (m < H && f >= 0) {
-            w = W1[(size_t)m * 198 + f];
-            if (f == 97 || f == 195) w = w / 15.0f;
+        if (unit < H) {
+            if (f == kFeatBias) w = b1[unit];
+            else if (f >= 0) w = (f == 97 || f == 195) ? W1[(size_t)unit * 198 + f] / 15.0f : W1[(size_t)unit * 198 + f];
         }
-        _Float16 a, b;
-        split16(ldexpf(w, e1), a, b);
-        const size_t base = ((size_t)(kb * T + t) * 2) * 64 * 8;
-        w1q[base + (size_t)l * 8 + i] = a;
-        w1q[base + 64 * 8 + (size_t)l * 8 + i] = b;
+        _Float16 hi, lo;
+        split16(ldexpf(w, e1), hi, lo);
+        w1q[((size_t)(kb * NT + t) * 64 + l) * 8 + i] = part ? lo : hi;
+    }
+    for (int idx = tid; idx < NT * 8 * 64; idx += 1024) {
+        const int l = idx & 63, j = (idx >> 6) & 7, t = idx >> 9;
+        const int unit = 16 * t + (j & 3) + 8 * (j >> 2) + 4 * (l >> 5);
+        wvq[idx] = unit < H ? ldexpf(wv[unit], -e1) : 0.0f;
     }
 }
 
@@ -773,7 +794,8 @@ __global__ void k_value_pack(const float* W1, const float* b1, const float* wv, 
 extern int bgx_internal_fail(hipError_t e);
 #define SCK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return bgx_internal_fail(_e); } while (0)
 
-static int value_tiles(int H) { return H <= 32 ? 1 : 2; }
+static int value_tiles(int H) { return H <= 32 ? 1 : 2; }   // f32 section (1-ply): 32-unit tiles
+static int value_tiles16(int H) { return (H + 15) / 16; }   // f16 section (2-ply): 16 units per tile
 
 template <typename K>
 static int persistent_grid(const bgx_engine* e, K kernel, int per_cu_cap) {
@@ -789,8 +811,7 @@ extern "C" {
 
 int bgx_value_packed_size(int32_t hidden) {
     if (hidden <= 0 || hidden > 64) return BGX_EINVAL;
-    const int T = value_tiles(hidden);
-    return sz_f32(T) + sz_f16(T);
+    return sz_f32(value_tiles(hidden)) + sz_f16(value_tiles16(hidden));
 }
 
 int bgx_value_pack(const float* W1, const float* b1, const float* wv, const float* bv, int32_t hidden, float* packed,
@@ -807,8 +828,9 @@ int bgx_value_pack(const float* W1, const float* b1, const float* wv, const floa
                        T, w1p, b1p, wvp, bvp);
     SCK(hipGetLastError());
     float* f16s = packed + n32;
-    hipLaunchKernelGGL(k_value_pack16, dim3(1), dim3(1024), 0, (hipStream_t)stream, W1, hidden, T, (int*)f16s,
-                       (_Float16*)(f16s + 4));
+    const int NT = value_tiles16(hidden);
+    hipLaunchKernelGGL(k_value_pack16, dim3(1), dim3(1024), 0, (hipStream_t)stream, W1, b1, wv, hidden, NT,
+                       (int*)f16s, (_Float16*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4);
     SCK(hipGetLastError());
     return BGX_OK;
 }
@@ -937,11 +959,11 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             if (const char* c = strchr(fs, ':')) S.cap_mid = atoi(c + 1);
         }
         const bool dbg = getenv("BGX_2PLY_DEBUG") != nullptr;
-        const int T = value_tiles(hidden);
-        const float* f16s = vpacked + sz_f32(T);
+        const int NT = value_tiles16(hidden);
+        const float* f16s = vpacked + sz_f32(value_tiles(hidden));
         const VNet vn = make_vnet(vpacked, hidden, value_bias);
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
-                   (const uint4*)(f16s + 4), vn.b1p, vn.wvp, (const int*)f16s, value_bias};
+                   (const uint4*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4, value_bias};
         const int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
         const int g_heavy = persistent_grid(e, kheavy, 32);
         const int g_list = persistent_grid(e, klist, 32);
@@ -970,7 +992,8 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         S.cap = E.cap = (unsigned long long)pcap;
         int g_eval = 0, ncu = 0;
         SCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device));
-        SCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&g_eval, T == 1 ? k_eval<1> : k_eval<2>, 64 * kEvalWaves, 0));
+        void (*keval)(EvalArgs) = NT == 1 ? k_eval<1> : NT == 2 ? k_eval<2> : NT == 3 ? k_eval<3> : k_eval<4>;
+        SCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&g_eval, keval, 64 * kEvalWaves, 0));
         g_eval = (g_eval > 0 ? g_eval : 1) * (ncu > 0 ? ncu : 256);
         if (!e->search_ev[0])
             for (hipEvent_t& ev : e->search_ev) SCK(hipEventCreate(&ev));
@@ -979,8 +1002,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         if (overlap && !e->search_side) SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
         SCK(hipEventRecord(e->search_ev[0], s));
         auto eval = [&](hipStream_t st) {
-            if (T == 1) hipLaunchKernelGGL(k_eval<1>, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
-            else hipLaunchKernelGGL(k_eval<2>, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
+            hipLaunchKernelGGL(keval, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
         };
         // retry rounds run few waves: every wave holding a block wastes its unused
         // part, and a round must leave pool for its jobs to finish (progress with any pool)
