@@ -176,6 +176,22 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float v
 int bgx_two_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float value_bias, int32_t* best_out,
                 float* bestq_out, float* q_out, uint64_t* stats_host, void* stream);
 
+/* ---- PPO update loss head (ppo_agent.py:268-305), fused ----
+ * For n rows: masked log-softmax of the logits (dtype 0 = fp32, 1 = fp16, row
+ * stride ld_logits; mask from the legal count in bytes 60-61 of each 64-byte
+ * lane record: log(1e-45) for illegal actions), ratio = exp(logp[action] -
+ * old_logp), clipped surrogate (eps_clip), value MSE, entropy.  Writes the
+ * gradients of  policy + c_value * value - c_entropy * entropy  (per-row losses,
+ * times grad_scale) with respect to the logits (dlogits, same dtype, row stride
+ * ld_dlogits) and the values (dvalues, same dtype), as torch autograd forms them,
+ * and adds the sums of the per-row policy loss, squared value error and entropy
+ * to sums[0..2] (double, device). */
+int bgx_ppo_head(const void* logits_dev, int32_t dtype, int64_t ld_logits, const void* values_dev,
+                 const uint8_t* records_dev, const int32_t* actions_dev, const float* old_logp_dev,
+                 const float* returns_dev, const float* adv_dev, int32_t n, int32_t n_actions, float eps_clip,
+                 float c_value, float c_entropy, float grad_scale, void* dlogits_dev, int64_t ld_dlogits,
+                 void* dvalues_dev, double* sums_dev, void* stream);
+
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
  * evaluation after it (k_eval, the MFMA kernel). */

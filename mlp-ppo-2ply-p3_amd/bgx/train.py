@@ -34,6 +34,10 @@ import torch.distributed as dist
 import torch.nn as nn
 from torch.amp import GradScaler, autocast
 
+import ctypes
+
+from . import _lib
+from ._lib import check
 from .engine import Engine, encode
 from .policy import PolicyNet, MASK_LOG
 from .ppo import (EPS_CLIP, GAMMA, LEARNING_RATE, NUM_EPOCHS, VALUE_LOSS_COEF, ENTROPY_COEF_START,
@@ -73,15 +77,54 @@ def features_and_masks(records: torch.Tensor, n_actions: int):
     return feats, legal
 
 
+class _PPOHead(torch.autograd.Function):
+    """The loss head of ppo_epoch on the HIP kernel bgx_ppo_head: forward computes
+    the per-row losses' sums AND the gradients w.r.t. logits and values (already
+    multiplied by `gscale` = GradScaler scale / n_total); backward hands them out.
+    Call .backward() on the (zero) output directly: the incoming gradient is
+    taken to be 1."""
+
+    @staticmethod
+    def forward(ctx, logits, values, records, actions, old_logp, returns, adv, coefs, sums):
+        eps, c_v, c_e, gscale = coefs
+        if logits.dtype not in (torch.float16, torch.float32) or values.dtype != logits.dtype:
+            raise TypeError(f"bgx_ppo_head: logits/values must be fp16 or fp32 alike, got {logits.dtype}/{values.dtype}")
+        logits, values = logits.contiguous(), values.contiguous()
+        n, A = logits.shape
+        dlog = torch.empty_like(logits)
+        dval = torch.empty_like(values)
+        L = _lib.load()
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        check(L.bgx_ppo_head(p(logits), 0 if logits.dtype == torch.float32 else 1, A, p(values),
+                             p(records), p(actions), p(old_logp), p(returns), p(adv), n, A, eps, c_v, c_e, gscale,
+                             p(dlog), A, p(dval), p(sums),
+                             ctypes.c_void_p(torch.cuda.current_stream(logits.device).cuda_stream)), "bgx_ppo_head")
+        ctx.save_for_backward(dlog, dval)
+        return logits.new_zeros((), dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        dlog, dval = ctx.saved_tensors
+        return dlog, dval, None, None, None, None, None, None, None
+
+
 def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_coef: float, group=None,
-              amp: bool = True):
+              amp: bool = True, fused: bool | None = None, step: bool = True):
     """One full-batch PPO epoch (ppo_agent.py:268-305) over `chunks` =
-    iterable of (features, legal_mask, actions, old_logp, returns, advantages),
-    with gradient accumulation and one all-reduce.  Returns loss parts."""
+    iterable of (features, legal_mask, actions, old_logp, returns, advantages
+    [, records]), with gradient accumulation and one all-reduce.  Returns loss
+    parts.  fused (default: on the GPU when the chunks carry their 64-byte
+    records): the loss head runs as one HIP kernel (bgx_ppo_head) instead of the
+    torch formulation below, which stays as its reference (tests compare them)."""
     optimizer.zero_grad(set_to_none=True)
     parts = torch.zeros(4, dtype=torch.float64)
-    dev_type = next(net.parameters()).device.type
-    for feats, legal, actions, old_logp, returns, adv in chunks:
+    dev = next(net.parameters()).device
+    dev_type = dev.type
+    if fused is None:
+        fused = dev_type == "cuda"
+    if fused:
+        return _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step)
+    for feats, legal, actions, old_logp, returns, adv, *_ in chunks:
         w = feats.shape[0] / n_total
         with autocast(device_type=dev_type, enabled=amp):
             logits, values = net(feats)
@@ -98,22 +141,49 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
         scaler.scale(loss * w).backward()
         parts += torch.tensor([policy_loss.item(), value_loss.item(), entropy.item(), loss.item()],
                               dtype=torch.float64) * w
-    allreduce_mean_([p.grad for p in net.parameters() if p.grad is not None], group)
-    scaler.step(optimizer)
-    scaler.update()
+    if step:
+        allreduce_mean_([p.grad for p in net.parameters() if p.grad is not None], group)
+        scaler.step(optimizer)
+        scaler.update()
     return parts
+
+
+def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step):
+    dev = next(net.parameters()).device
+    if scaler.is_enabled():
+        scaler.scale(torch.ones((), device=dev))          # initialises the scale tensor lazily
+        scale = scaler.get_scale()
+    else:
+        scale = 1.0
+    sums = torch.zeros(3, dtype=torch.float64, device=dev)
+    coefs = (EPS_CLIP, VALUE_LOSS_COEF, float(entropy_coef), float(scale) / n_total)
+    for feats, legal, actions, old_logp, returns, adv, records in chunks:
+        with autocast(device_type=dev.type, enabled=amp):
+            logits, values = net(feats)
+        out = _PPOHead.apply(logits, values, records.contiguous(), actions.to(torch.int32).contiguous(),
+                             old_logp.float().contiguous(), returns.float().contiguous(), adv.float().contiguous(),
+                             coefs, sums)
+        out.backward()
+    if step:
+        allreduce_mean_([p.grad for p in net.parameters() if p.grad is not None], group)
+        scaler.step(optimizer)
+        scaler.update()
+    pol, val, ent = (sums / n_total).tolist()
+    tot = pol + VALUE_LOSS_COEF * val - entropy_coef * ent
+    return torch.tensor([pol, val, ent, tot], dtype=torch.float64)
 
 
 class PPOTrainer:
     def __init__(self, batch: int = 65536, horizon: int = 64, hidden: int = 128, n_actions: int = 500,
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
-                 chunk: int = 1 << 20):
+                 chunk: int = 1 << 20, fused: bool | None = None):
         self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.group = process_group
         self.rank = dist.get_rank(process_group) if _world(process_group) > 1 else 0
         self.B, self.T, self.A = batch, horizon, n_actions
         self.returns_mode = returns
         self.chunk = chunk
+        self.fused = (self.dev.type == "cuda") if fused is None else fused
         self.eng = Engine(batch=batch, max_moves=n_actions, seed=seed * 1_000_003 + self.rank, dice="philox",
                           auto_reset=True, device=self.dev)
         torch.manual_seed(seed)
@@ -186,12 +256,17 @@ class PPOTrainer:
         def chunks():
             for s in range(0, N, self.chunk):
                 e = min(N, s + self.chunk)
-                f, legal = features_and_masks(recs[s:e], self.A)
-                yield f, legal, acts[s:e], old[s:e], R[s:e], adv[s:e]
+                if self.fused:      # the loss kernel reads the legal counts from the records
+                    f = encode(recs[s:e, :52].contiguous(), recs[s:e, 52].contiguous())
+                    legal = None
+                else:
+                    f, legal = features_and_masks(recs[s:e], self.A)
+                yield f, legal, acts[s:e], old[s:e], R[s:e], adv[s:e], recs[s:e]
 
         parts = torch.zeros(4, dtype=torch.float64)
         for _ in range(NUM_EPOCHS):
-            parts += ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group)
+            parts += ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
+                               fused=self.fused)
         progress = min(1.0, self.total_episodes / ENTROPY_ANNEAL_EPISODES)       # ppo_agent.py:193-197
         self.entropy_coef = ENTROPY_COEF_START - progress * (ENTROPY_COEF_START - ENTROPY_COEF_END)
         p = (parts / NUM_EPOCHS).tolist()
