@@ -389,6 +389,7 @@ struct Gen {
     SlotPtr tab;
     uint4* memo2;       // LDS memo tables (nullptr = no pruning)
     uint4* memo3;
+    int memo_share = 3;  // MEMO_KIND 2: memo entries may take memo_share/8 of the table's capacity
     int n_memo2, n_memo3;
     Sink sink;
     int pl;
@@ -544,7 +545,7 @@ struct Gen {
         int room;
         if (MEMO_KIND == 0) room = ((7 << LOGM) / 8) - nm;
         else if (MEMO_KIND == 1) room = ((7 << kLogCMemo) / 8) - n_memo2 - n_memo3;
-        else room = min(((7 << LOGM) / 8) - nm, cap_unique / 3 - n_memo2 - n_memo3);
+        else room = min(((7 << LOGM) / 8) - nm, cap_unique * memo_share / 8 - n_memo2 - n_memo3);
         while (n > room && rec) { rec &= ~(1ull << (63 - __clzll((long long)rec))); --n; }
         uint64_t kept = rec;
         if (rec) {

@@ -192,6 +192,7 @@ struct S2 {
     const int32_t* list_count;
     int32_t* err;
     int cap_light, cap_heavy, cap_mid;   // unique-entry capacity of the LDS tables (tests shrink them)
+    int memo_mask, memo_share;           // revisit memo at depth 2 (bit 0) / 3 (bit 1); in-table share /8
 };
 
 __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
@@ -267,8 +268,9 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, int r, int q, cons
     Gen<LOG, SlotPtr, KeySink, MK < 0 ? 0 : MK> g;
     g.tab = tab; g.pl = q; g.cap_unique = cap_unique; g.blocked = blocked;
     if (MK == 2) memo = (uint4*)tab;    // non-null: pruning on (entries live in tab)
-    g.memo2 = MK >= 0 && dbl ? memo : nullptr;
-    g.memo3 = MK >= 0 && dbl ? (MK == 1 ? memo : memo + (1 << kLogMemo2)) : nullptr;
+    g.memo2 = MK >= 0 && dbl && (S.memo_mask & 1) ? memo : nullptr;
+    g.memo3 = MK >= 0 && dbl && (S.memo_mask & 2) ? (MK == 1 ? memo : memo + (1 << kLogMemo2)) : nullptr;
+    g.memo_share = S.memo_share;
     g.sink = sink;
     g.sink.job = (uint32_t)job;
     g.sink.lost = false;
@@ -934,7 +936,9 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         SCK(hipGetLastError());
         S2 S{rowrec, 0, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
-             retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>()};
+             retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>(), 3, 3};
+        if (const char* v = getenv("BGX_2PLY_MEMO")) S.memo_mask = atoi(v);
+        if (const char* v = getenv("BGX_2PLY_MEMO_SHARE")) S.memo_share = atoi(v);
         // doubles enumerator: dedup table 2^LOG slots + revisit memo kind (BGX_2PLY_HEAVY=LOG:MK)
         int hlog = 9, hmk = 2, hwpe = 0;
         if (const char* hv = getenv("BGX_2PLY_HEAVY")) {
