@@ -511,17 +511,33 @@ __device__ __forceinline__ uint32_t f16_pair(uint32_t ab, float s0, float s1) {
     return __builtin_bit_cast(uint32_t, r);
 }
 
+// packed u16x2 ops (clang scalarises them from vector code into cmp/cndmask pairs)
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    __asm__("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_mul_lo_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    __asm__("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // the four units of two points with counts (a, b) (immutable_board.py:180-195) as
 // f16 pairs [u_k(a), u_k(b)], k = 0..3: n>=1, n>=2, n>=3, (n-3)/2 if n>=3
 __device__ __forceinline__ uint4 units_pair(uint32_t byte) {
-    const u16x2 x = __builtin_bit_cast(u16x2, (byte & 15u) | ((byte & 0xF0u) << 12));
-    const u16x2 one = {1, 1}, two = {2, 2}, three = {3, 3}, f1 = {0x3C00, 0x3C00};
-    const u16x2 u0 = __builtin_elementwise_min(x, one) * f1;
-    const u16x2 u1 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(x, one), one) * f1;
-    const u16x2 u2 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(x, two), one) * f1;
-    const uint32_t u3 = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(x, three));
-    return make_uint4(__builtin_bit_cast(uint32_t, u0), __builtin_bit_cast(uint32_t, u1),
-                      __builtin_bit_cast(uint32_t, u2), f16_pair(u3, 0.5f, 0.5f));
+    const uint32_t x = (byte & 15u) | ((byte & 0xF0u) << 12);
+    const uint32_t one = 0x00010001u, f1 = 0x3C003C00u;
+    const uint32_t x1 = pk_subsat_u16(x, one), x2 = pk_subsat_u16(x1, one), x3 = pk_subsat_u16(x2, one);
+    const uint32_t u0 = pk_mul_lo_u16(pk_min_u16(x, one), f1);
+    const uint32_t u1 = pk_mul_lo_u16(pk_min_u16(x1, one), f1);
+    const uint32_t u2 = pk_mul_lo_u16(pk_min_u16(x2, one), f1);
+    return make_uint4(u0, u1, u2, f16_pair(x3, 0.5f, 0.5f));
 }
 
 // B operand of k-block kb for this lane's half h (permuted K order, kperm)
