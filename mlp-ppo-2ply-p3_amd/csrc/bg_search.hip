@@ -984,8 +984,10 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const VNet vn = make_vnet(vpacked, hidden, value_bias);
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4, value_bias};
-        const int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
-        const int g_heavy = persistent_grid(e, kheavy, 32);
+        int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
+        int g_heavy = persistent_grid(e, kheavy, 32);
+        if (const char* v = getenv("BGX_2PLY_HGRID")) g_heavy = atoi(v) > 0 ? atoi(v) : g_heavy;
+        if (const char* v = getenv("BGX_2PLY_LGRID")) g_light = atoi(v) > 0 ? atoi(v) : g_light;
         const int g_list = persistent_grid(e, klist, 32);
         const int g_t0 = persistent_grid(e, k_enum_tier<10, 0>, 32);
         const int g_mid = persistent_grid(e, k_enum_tier<kLogMid, 1>, 32);
@@ -1019,7 +1021,15 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             for (hipEvent_t& ev : e->search_ev) SCK(hipEventCreate(&ev));
         const char* ov = getenv("BGX_2PLY_OVERLAP");    // "0": enumerators back to back (A/B)
         const bool overlap = !(ov && ov[0] == '0');
-        if (overlap && !e->search_side) SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
+        if (overlap && !e->search_side) {
+            // BGX_2PLY_SIDE_PRIO = hi / lo: the non-doubles enumerator's stream priority (A/B)
+            const char* pr = getenv("BGX_2PLY_SIDE_PRIO");
+            int lo = 0, hi = 0;
+            if (pr && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && (pr[0] == 'h' || pr[0] == 'l'))
+                SCK(hipStreamCreateWithPriority(&e->search_side, hipStreamNonBlocking, pr[0] == 'h' ? hi : lo));
+            else
+                SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
+        }
         SCK(hipEventRecord(e->search_ev[0], s));
         auto eval = [&](hipStream_t st) {
             hipLaunchKernelGGL(keval, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);

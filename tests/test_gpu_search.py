@@ -129,3 +129,36 @@ def test_two_ply_overflow_tiers(setup, monkeypatch, caps, heavy):
     assert st2["leaves"] == st["leaves"]
     assert torch.equal(torch.nan_to_num(q2, 7.0), torch.nan_to_num(q, 7.0))
     assert torch.equal(best2, best)
+
+
+def test_two_ply_full_batch_paths_agree(monkeypatch):
+    """C4 at full size (B = 65,536 roots after 60 self-play steps): the doubles
+    enumerator with its revisit memo inside a 512-slot table and with a
+    1,024-slot table plus separate memo tables (different tier traffic, pruning
+    and pool block order) give bit-identical Q, the same choices and the same
+    surviving-leaf counts; every choice is a legal move and every Q is finite."""
+    import bgx
+    from bgx.policy import PolicyNet
+    from bgx.search import ValueHead, two_ply
+    torch.manual_seed(0)
+    net = PolicyNet().cuda()
+    eng = bgx.Engine(batch=65536, max_moves=500, seed=77, dice="philox", auto_reset=True)
+    eng.reset(want_obs=False)
+    for i in range(60):
+        a, _, _ = net.act(net.rollout_inputs(eng), seed=5, step=i)
+        eng.step(a, want_obs=False, want_info=False)
+    vh = ValueHead(PolicyNet(hidden_size=40).cuda())
+    b1, q1, Q1, s1 = two_ply(eng, vh, want_q=True)
+    monkeypatch.setenv("BGX_2PLY_HEAVY", "10:0")
+    b2, q2, Q2, s2 = two_ply(eng, vh, want_q=True)
+    assert s1 == s2
+    assert torch.equal(torch.nan_to_num(Q1, 7.0), torch.nan_to_num(Q2, 7.0))
+    assert torch.equal(b1, b2) and torch.equal(q1, q2)
+    n = eng.n_moves()
+    assert bool(((b1 < n) | (n == 0)).all())
+    has = n > 0
+    assert bool(torch.isfinite(q1[has]).all())
+    col = torch.arange(Q1.shape[1], device="cuda")[None, :]
+    assert bool(torch.isfinite(Q1[col < n[:, None]]).all())
+    assert s1["afterstates"] == int(n.sum()) and s1["jobs"] == 21 * s1["afterstates"]
+    assert eng.error() == 0
