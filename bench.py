@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--burn-in", type=int, default=150,
                     help="untimed steps before warmup so the game population reaches its steady mix "
                          "(openings are cheaper than mid-game positions)")
+    ap.add_argument("--host-mirror", action="store_true",
+                    help="C3: also copy every rollout row to pinned host memory (PCIe-inclusive rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
@@ -234,15 +236,24 @@ def main():
     net = PolicyNet(hidden_size=128, action_size=500).to(dev)
     net.pack()
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
-    ring = 8
-    pins = [{
-        "boards": torch.empty(ring, Bs, 64, dtype=torch.uint8).pin_memory(),
-        "act": torch.empty(ring, Bs, dtype=torch.int32).pin_memory(),
-        "logp": torch.empty(ring, Bs, dtype=torch.float32).pin_memory(),
-        "value": torch.empty(ring, Bs, dtype=torch.float32).pin_memory(),
-        "reward": torch.empty(ring, Bs, dtype=torch.float32).pin_memory(),
-        "done": torch.empty(ring, Bs, dtype=torch.uint8).pin_memory(),
+    # Rollout storage: a device-resident ring of T rollout rows per shard (the
+    # PPOTrainer layout, bgx/train.py): records, actions, log-probs, values,
+    # rewards, dones — 81 B per lane-step written straight into HBM by the
+    # kernels.  --host-mirror additionally streams every row to pinned host
+    # memory on a side stream (the reference keeps its rollout in host lists);
+    # that copy runs as blit kernels that share the CUs with the policy kernel.
+    ring = 32
+    kw = dict(device=dev)
+    bufs = [{
+        "records": torch.empty(ring, Bs, 64, dtype=torch.uint8, **kw),
+        "act": torch.empty(ring, Bs, dtype=torch.int32, **kw),
+        "logp": torch.empty(ring, Bs, dtype=torch.float32, **kw),
+        "value": torch.empty(ring, Bs, dtype=torch.float32, **kw),
+        "reward": torch.empty(ring, Bs, dtype=torch.float32, **kw),
+        "done": torch.empty(ring, Bs, dtype=torch.uint8, **kw),
     } for _ in range(S)]
+    pins = [{k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in b.items()}
+            for b in bufs] if args.host_mirror else None
     copy_streams = [torch.cuda.Stream(dev) for _ in range(S)]
     counts = [torch.empty(Bs, dtype=torch.int16, device=dev) for _ in range(S)]
     gen = torch.Generator(device=dev).manual_seed(99 + rank)
@@ -263,25 +274,25 @@ def main():
                     e1.record(st)
                     ev_pairs.append((e0, e1))
                 return
-            rec = net.rollout_inputs(e)                         # int8 lane boards (no fp32 obs round trip)
-            act, logp, value = net.act(rec, seed=4242 + rank * 16 + k, step=i)   # fused HIP policy step
+            b, slot = bufs[k], i % ring
+            rec = e.records(out=b["records"][slot])              # int8 lane boards (no fp32 obs round trip)
+            net.act(rec, seed=4242 + rank * 16 + k, step=i,        # fused HIP policy step
+                    out=(b["act"][slot], b["logp"][slot], b["value"][slot]))
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
-            _, rew, done, _ = e.step(act, want_obs=False, want_info=False)
+            e.step(b["act"][slot], want_obs=False, want_info=False, out=(b["reward"][slot], b["done"][slot]))
             if timed:
                 e1.record(st)
                 ev_pairs.append((e0, e1))
-            # rollout record -> pinned host ring (side stream, overlapped)
-            slot = i % ring
-            cs = copy_streams[k]
-            cs.wait_stream(st)
-            with torch.cuda.stream(cs):
-                for name, v in (("boards", rec), ("act", act), ("logp", logp), ("value", value),
-                                ("reward", rew), ("done", done)):
-                    pins[k][name][slot].copy_(v, non_blocking=True)
-                    v.record_stream(cs)
-            st.wait_stream(cs) if slot == ring - 1 else None
+            if pins is not None:                                  # optional pinned-host mirror (side stream)
+                cs = copy_streams[k]
+                cs.wait_stream(st)
+                with torch.cuda.stream(cs):
+                    for name in b:
+                        pins[k][name][slot].copy_(b[name][slot], non_blocking=True)
+                if slot == ring - 1:
+                    st.wait_stream(cs)                            # the ring wraps: rows must be on the host
 
     def step(timed: bool):
         i = state["i"]
@@ -349,7 +360,9 @@ def main():
         "data": "synthetic self-play (Philox dice), random-init BackgammonPolicyNetwork weights",
         "burn_in": args.burn_in,
         "config": {"workload": (f"C3: B={B} games/GPU PPO rollout step (policy 198->128->{{500,1}} + masked "
-                                "sample + env.step)") if args.workload == "c3" else
+                                "sample + env.step, rollout rows stored to an HBM ring"
+                                + (" + pinned-host mirror" if args.host_mirror else "") + ")")
+                   if args.workload == "c3" else
                    f"C1-on-GPU: B={B} games/GPU random legal policy env.step",
                    "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
                    "parallelism": f"dp{ws} (independent game shards)", "shards_per_gpu": S,

@@ -103,18 +103,27 @@ class Engine:
               "bgx_reset")
         return self.obs
 
-    def step(self, actions: torch.Tensor, want_obs: bool = True, want_info: bool = True):
+    def step(self, actions: torch.Tensor, want_obs: bool = True, want_info: bool = True, out=None):
         """Advance every lane by one BackgammonEnv.step; returns (obs, reward, done, info)
         views of engine-owned buffers (overwritten by the next step).  want_obs=False
-        skips the fp32 observation write (rollouts that keep int8 boards)."""
+        skips the fp32 observation write (rollouts that keep int8 boards); `out` =
+        (reward f32[B], done u8[B]) tensors the step writes instead (rows of a
+        device-resident rollout buffer)."""
         a = actions
         if not (isinstance(a, torch.Tensor) and a.device == self.device and a.dtype == torch.int32
                 and a.is_contiguous()):
             a = torch.as_tensor(a).to(device=self.device, dtype=torch.int32).contiguous()
-        check(self._lib.bgx_step(self._h, _ptr(a), _ptr(self.obs) if want_obs else None, _ptr(self.reward),
-                                 _ptr(self.done), _ptr(self.info) if want_info else None, self._stream()),
+        reward, done = self.reward, self.done
+        if out is not None:
+            reward, done = out
+            if (reward.dtype != torch.float32 or done.dtype != torch.uint8 or reward.device != self.device
+                    or done.device != self.device or not reward.is_contiguous() or not done.is_contiguous()
+                    or reward.numel() != self.batch or done.numel() != self.batch):
+                raise ValueError("step: out must be contiguous (float32[B], uint8[B]) on the engine's device")
+        check(self._lib.bgx_step(self._h, _ptr(a), _ptr(self.obs) if want_obs else None, _ptr(reward),
+                                 _ptr(done), _ptr(self.info) if want_info else None, self._stream()),
               "bgx_step")
-        return self.obs, self.reward, self.done, self.info
+        return self.obs, reward, done, self.info
 
     # --------------------------------------------------------------- state --
     def lanes(self, lane0: int = 0, n: int | None = None):

@@ -65,10 +65,12 @@ class PolicyNet(nn.Module):
 
     @torch.no_grad()
     def act(self, records: torch.Tensor, seed: int = 0, step: int = 0, greedy: bool = False,
-            packed: torch.Tensor | None = None, want_logits: bool = False):
+            packed: torch.Tensor | None = None, want_logits: bool = False, out=None):
         """select_action (ppo_agent.py:138-191) for every lane in ONE fused HIP
         kernel (encode -> MLP on MFMA -> masked softmax -> sample).  Returns
-        (action int32[B], log_prob f32[B], value f32[B][, logits])."""
+        (action int32[B], log_prob f32[B], value f32[B][, logits]); `out` =
+        (action, log_prob, value) tensors to write instead (e.g. rows of a
+        device-resident rollout buffer)."""
         L = _lib.load()
         packed = packed if packed is not None else getattr(self, "_packed", None)
         if packed is None:
@@ -77,9 +79,15 @@ class PolicyNet(nn.Module):
         r = records.contiguous()
         n = r.shape[0]
         dev = r.device
-        act = torch.empty(n, dtype=torch.int32, device=dev)
-        logp = torch.empty(n, dtype=torch.float32, device=dev)
-        val = torch.empty(n, dtype=torch.float32, device=dev)
+        if out is not None:
+            act, logp, val = out
+            for t, dt in zip(out, (torch.int32, torch.float32, torch.float32)):
+                if t.dtype != dt or t.device != dev or not t.is_contiguous() or t.numel() != n:
+                    raise ValueError("act: out tensors must be contiguous int32/f32/f32 [n] on the records' device")
+        else:
+            act = torch.empty(n, dtype=torch.int32, device=dev)
+            logp = torch.empty(n, dtype=torch.float32, device=dev)
+            val = torch.empty(n, dtype=torch.float32, device=dev)
         logits = torch.empty(n, 32 * ((A + 32) // 32), dtype=torch.float32, device=dev) if want_logits else None
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         check(L.bgx_policy_act(_ptr(r), n, _ptr(packed), H, A, int(seed) & (2**64 - 1), int(step) & 0xFFFFFFFF,

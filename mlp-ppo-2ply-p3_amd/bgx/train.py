@@ -217,14 +217,11 @@ class PPOTrainer:
         buf = self.buf
         for t in range(self.T):
             self.eng.records(out=buf["records"][t])
-            a, lp, v = self.net.act(buf["records"][t], seed=self.seed * 7919 + self.rank, step=self.step_counter)
+            self.net.act(buf["records"][t], seed=self.seed * 7919 + self.rank, step=self.step_counter,
+                         out=(buf["actions"][t], buf["logp"][t], buf["values"][t]))
             self.step_counter += 1
-            buf["actions"][t].copy_(a)
-            buf["logp"][t].copy_(lp)
-            buf["values"][t].copy_(v)
-            _, r, d, _ = self.eng.step(a, want_obs=False, want_info=False)
-            buf["rewards"][t].copy_(r)
-            buf["dones"][t].copy_(d)
+            self.eng.step(buf["actions"][t], want_obs=False, want_info=False,
+                          out=(buf["rewards"][t], buf["dones"][t]))
             if self.pinned is not None:
                 cur = torch.cuda.current_stream(self.dev)
                 self.copy_stream.wait_stream(cur)

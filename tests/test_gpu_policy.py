@@ -107,3 +107,37 @@ def test_policy_sampling_distribution(bgx):
     chi2 = ((freq[keep] - p[keep]) ** 2 / p[keep]).sum() * N
     dof = int(keep.sum()) - 1
     assert chi2 < dof + 6 * np.sqrt(2 * dof) + 10, (chi2, dof)
+
+
+def test_policy_sampling_no_legal_moves(bgx):
+    """A row with no legal move samples from the softmax over all 500 masked
+    logits (ppo_agent.py:160-170 with an all-zero mask).  The kernel draws such
+    rows lane-parallel; rows with legal moves in the same waves are unaffected."""
+    from bgx.policy import PolicyNet, masked_probs
+    torch.manual_seed(2)
+    net = PolicyNet(hidden_size=128).cuda()
+    with torch.no_grad():
+        net.action_head.weight.mul_(8.0)
+    eng = bgx.Engine(batch=64, dice="philox", seed=13)
+    eng.reset()
+    rec = eng.records()
+    N = 200_000
+    reps = rec[:2].repeat(N // 2, 1).contiguous()
+    reps[0::2, 60] = 0                         # even rows: no legal move
+    reps[0::2, 61] = 0
+    a, logp, _ = net.act(reps, seed=321, step=4)
+    x = bgx.encode(rec[:1, :52].contiguous(), rec[:1, 52].contiguous())
+    with torch.no_grad():
+        lg, _ = net(x)
+    p = masked_probs(lg, torch.zeros(1, 500, device="cuda"))[0].cpu().numpy()
+    lsm = torch.log_softmax(lg + (torch.zeros(1, 500, device="cuda") + 1e-45).log(), -1)[0]
+    az = a[0::2].long()
+    # every logit carries the -103.28 mask here: |z| ~ 110, where one fp32 ulp is 7.6e-6
+    assert (logp[0::2] - lsm[az]).abs().max().item() < 4 * TOL
+    freq = np.bincount(az.cpu().numpy(), minlength=500)[:500] / (N // 2)
+    keep = p * (N // 2) > 20
+    chi2 = ((freq[keep] - p[keep]) ** 2 / p[keep]).sum() * (N // 2)
+    dof = int(keep.sum()) - 1
+    assert chi2 < dof + 6 * np.sqrt(2 * dof) + 10, (chi2, dof)
+    c1 = int(rec[1, 60]) | (int(rec[1, 61]) << 8)
+    assert c1 > 0 and torch.all(a[1::2] < c1)
