@@ -275,9 +275,10 @@ def main():
                     ev_pairs.append((e0, e1))
                 return
             b, slot = bufs[k], i % ring
-            rec = e.records(out=b["records"][slot])              # int8 lane boards (no fp32 obs round trip)
-            net.act(rec, seed=4242 + rank * 16 + k, step=i,        # fused HIP policy step
-                    out=(b["act"][slot], b["logp"][slot], b["value"][slot]))
+            # fused HIP policy step on the engine's lane records in place; it also
+            # stores them (int8 boards, no fp32 obs round trip) as the rollout row
+            net.act(e, seed=4242 + rank * 16 + k, step=i,
+                    out=(b["act"][slot], b["logp"][slot], b["value"][slot]), records_out=b["records"][slot])
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)

@@ -153,6 +153,15 @@ int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed_de
                    uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out, float* value_out,
                    float* logits_out, void* stream);
 
+/* bgx_policy_act that also writes each row's 64-byte input record to
+ * records_out uint8[n][64] (the rollout's stored observation,
+ * select_action appends the state to memory, ppo_agent.py:176-185), so a rollout reads the
+ * engine's lane buffer (bgx_buffers.lanes) in place with no separate copy.
+ * records_out may be NULL (then identical to bgx_policy_act). */
+int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packed_dev, int32_t hidden,
+                       int32_t n_actions, uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out,
+                       float* logp_out, float* value_out, float* logits_out, uint8_t* records_out, void* stream);
+
 /* ---- value head search: V(x) = value_head(relu(fc1 x)), H <= 64 ----
  * bgx_value_pack packs fc1.weight [H][198], fc1.bias [H], value_head.weight [H],
  * value_head.bias [1] into bgx_value_packed_size(H) floats (MFMA operand order);

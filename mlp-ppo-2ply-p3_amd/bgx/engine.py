@@ -70,6 +70,16 @@ class Engine:
                 pass
             self._h = None
 
+    def lanes_ptr(self) -> int:
+        """Device address of the engine's lane records (uint8[B][64], the
+        bgx_buffers.lanes layout that records() copies): a consumer on the
+        engine's stream may read them in place (e.g. PolicyNet.act(engine))."""
+        if getattr(self, "_lanes_ptr", None) is None:
+            b = _lib.BgxBuffers()
+            check(self._lib.bgx_engine_buffers(self._h, ctypes.byref(b)), "bgx_engine_buffers")
+            self._lanes_ptr = int(b.lanes)
+        return self._lanes_ptr
+
     # ------------------------------------------------------------ plumbing --
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)

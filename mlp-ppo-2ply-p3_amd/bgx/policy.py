@@ -65,20 +65,28 @@ class PolicyNet(nn.Module):
 
     @torch.no_grad()
     def act(self, records: torch.Tensor, seed: int = 0, step: int = 0, greedy: bool = False,
-            packed: torch.Tensor | None = None, want_logits: bool = False, out=None):
+            packed: torch.Tensor | None = None, want_logits: bool = False, out=None,
+            records_out: torch.Tensor | None = None):
         """select_action (ppo_agent.py:138-191) for every lane in ONE fused HIP
         kernel (encode -> MLP on MFMA -> masked softmax -> sample).  Returns
         (action int32[B], log_prob f32[B], value f32[B][, logits]); `out` =
         (action, log_prob, value) tensors to write instead (e.g. rows of a
-        device-resident rollout buffer)."""
+        device-resident rollout buffer).  `records` may be a bgx.Engine: its
+        lane records are read in place; `records_out` (uint8[B, 64]) then
+        receives the kernel's copy of them (the rollout's stored state)."""
         L = _lib.load()
         packed = packed if packed is not None else getattr(self, "_packed", None)
         if packed is None:
             packed = self.pack()
         H, A = self.fc1.out_features, self.action_head.out_features
-        r = records.contiguous()
-        n = r.shape[0]
-        dev = r.device
+        if isinstance(records, torch.Tensor):
+            r = records.contiguous()
+            rptr, n, dev = r.data_ptr(), r.shape[0], r.device
+        else:                                              # a bgx.Engine: lane records in place
+            rptr, n, dev = records.lanes_ptr(), records.batch, records.device
+        if records_out is not None and (records_out.dtype != torch.uint8 or records_out.device != dev
+                                        or not records_out.is_contiguous() or records_out.numel() != n * 64):
+            raise ValueError("act: records_out must be a contiguous uint8[n, 64] tensor on the records' device")
         if out is not None:
             act, logp, val = out
             for t, dt in zip(out, (torch.int32, torch.float32, torch.float32)):
@@ -90,9 +98,10 @@ class PolicyNet(nn.Module):
             val = torch.empty(n, dtype=torch.float32, device=dev)
         logits = torch.empty(n, 32 * ((A + 32) // 32), dtype=torch.float32, device=dev) if want_logits else None
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        check(L.bgx_policy_act(_ptr(r), n, _ptr(packed), H, A, int(seed) & (2**64 - 1), int(step) & 0xFFFFFFFF,
-                               int(bool(greedy)), _ptr(act), _ptr(logp), _ptr(val), _ptr(logits), s),
-              "bgx_policy_act")
+        check(L.bgx_policy_act_rec(ctypes.c_void_p(rptr), n, _ptr(packed), H, A, int(seed) & (2**64 - 1),
+                                   int(step) & 0xFFFFFFFF, int(bool(greedy)), _ptr(act), _ptr(logp), _ptr(val),
+                                   _ptr(logits), _ptr(records_out), s),
+              "bgx_policy_act_rec")
         if want_logits:
             return act, logp, val, logits
         return act, logp, val

@@ -216,9 +216,8 @@ class PPOTrainer:
         self.net.pack()
         buf = self.buf
         for t in range(self.T):
-            self.eng.records(out=buf["records"][t])
-            self.net.act(buf["records"][t], seed=self.seed * 7919 + self.rank, step=self.step_counter,
-                         out=(buf["actions"][t], buf["logp"][t], buf["values"][t]))
+            self.net.act(self.eng, seed=self.seed * 7919 + self.rank, step=self.step_counter,
+                         out=(buf["actions"][t], buf["logp"][t], buf["values"][t]), records_out=buf["records"][t])
             self.step_counter += 1
             self.eng.step(buf["actions"][t], want_obs=False, want_info=False,
                           out=(buf["rewards"][t], buf["dones"][t]))

@@ -399,6 +399,12 @@ struct bgx_engine {
     int32_t* perm;        // dispatch order for k_step (Philox mode), built by k_order
     bool perm_valid;
     int32_t* order_cnt;   // k_order_count -> k_order_scatter, [B/1024+1][kClasses]
+    // overflow counters, two 16-byte sets: a Philox step uses set `ovf_parity`
+    // (Args::ovf_count) and its k_order_count zeroes the other set for the next
+    // step, so the step needs no separate memset launch
+    int32_t* ovf_base;
+    int ovf_parity;
+    bool ovf_next_zeroed;
     uint64_t seed;
     // bg_search.hip workspace (grown on demand)
     void* search_ws;

@@ -96,9 +96,10 @@ __device__ __forceinline__ int order_class(const uint8_t* cls, int i, int B) {
 }
 
 // pass 1: cnt[b][c] = lanes of class c in block b
-__global__ __launch_bounds__(1024) void k_order_count(const uint8_t* cls, int32_t* cnt, int B) {
+__global__ __launch_bounds__(1024) void k_order_count(const uint8_t* cls, int32_t* cnt, int B, int32_t* zero_next) {
     __shared__ int sc[kClasses];
     const int t = threadIdx.x, i = blockIdx.x * 1024 + t;
+    if (blockIdx.x == 0 && t < 4) zero_next[t] = 0;     // the next step's overflow counters
     if (t < kClasses) sc[t] = 0;
     __syncthreads();
     const int c = order_class(cls, i, B);
@@ -388,7 +389,9 @@ int bgx_internal_fail(hipError_t e) { return fail(e); }
 
 static void launch_order(bgx_engine* e, hipStream_t s) {
     const int nblk = (e->a.B + 1023) / 1024;
-    hipLaunchKernelGGL(k_order_count, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->a.B);
+    hipLaunchKernelGGL(k_order_count, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->a.B,
+                       e->ovf_base + 4 * (e->ovf_parity ^ 1));
+    e->ovf_next_zeroed = true;
     hipLaunchKernelGGL(k_order_scatter, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->perm, e->a.B, nblk);
     e->perm_valid = true;
 }
@@ -467,7 +470,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     alloc((void**)&A.mt, (dice_mode == BGX_DICE_MT_SHARED ? 1 : (dice_mode == BGX_DICE_MT_LANE ? B : 1)) * kMtWords * 4);
     alloc((void**)&A.ctr, B * 8);
     alloc((void**)&A.shared_rolls, B * 4);
-    alloc((void**)&A.ovf_count, 16);
+    alloc((void**)&e->ovf_base, 32);
+    A.ovf_count = e->ovf_base;
     alloc((void**)&A.ovf_queue, 2 * B * 4);
     alloc((void**)&A.err, 16);
     alloc((void**)&e->slow_tables, (size_t)kSlowWaves * ((size_t)16 << kLogSlotsSlow));
@@ -480,7 +484,7 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     }
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }
     if (hipMemset(A.lanes, 0, B * 64) != hipSuccess || hipMemset(A.ctr, 0, B * 8) != hipSuccess ||
-        hipMemset(A.ovf_count, 0, 16) != hipSuccess || hipMemset(A.err, 0, 16) != hipSuccess ||
+        hipMemset(e->ovf_base, 0, 32) != hipSuccess || hipMemset(A.err, 0, 16) != hipSuccess ||
         hipMemset(A.n_total, 0, B * 4) != hipSuccess || (A.cls && hipMemset(A.cls, 0, B) != hipSuccess)) {
         bgx_engine_destroy(e);
         return fail(hipGetLastError());
@@ -498,7 +502,7 @@ int bgx_engine_destroy(bgx_engine* e) {
     if (!e) return BGX_EINVAL;
     (void)hipSetDevice(e->device);
     Args& A = e->a;
-    void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, A.ovf_count, A.ovf_queue, A.err,
+    void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, e->ovf_base, A.ovf_queue, A.err,
                     e->slow_tables, e->search_ws, e->search_pool, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (hipEvent_t ev : e->search_ev) if (ev) (void)hipEventDestroy(ev);
@@ -572,7 +576,13 @@ int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void*
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
-    CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
+    if (e->ovf_next_zeroed) {             // the previous step's k_order_count zeroed the other set
+        e->ovf_parity ^= 1;
+        A.ovf_count = e->ovf_base + 4 * e->ovf_parity;
+        e->ovf_next_zeroed = false;
+    } else {
+        CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
+    }
     if (A.dice_mode == BGX_DICE_MT_SHARED) {
         LAUNCH_LOG(e, k_reset, dim3(A.B), s, A, lane_mask_dev, obs_dev, 1);
         hipLaunchKernelGGL(k_shared_dice, dim3(1), dim3(64), 0, s, A);
@@ -593,7 +603,13 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
-    CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
+    if (e->ovf_next_zeroed) {             // the previous step's k_order_count zeroed the other set
+        e->ovf_parity ^= 1;
+        A.ovf_count = e->ovf_base + 4 * e->ovf_parity;
+        e->ovf_next_zeroed = false;
+    } else {
+        CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
+    }
     if (A.dice_mode == BGX_DICE_MT_SHARED) {
         hipLaunchKernelGGL((k_step<1, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
                            info_dev, 0);

@@ -83,6 +83,9 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 __device__ __forceinline__ float fast_ln(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 
+// gumbel() below is at most -log(2^-24) = 16.64 (u <= 1 - 2^-24)
+constexpr float kGumbelMax = 17.0f;
+
 // Gumbel(0,1) = -log(E), E = -log(u) ~ Exp(1), u = ((w >> 9) + 1/2) 2^-23 in (0,1).
 // For u close to 1, -log(u) = v + v^2/2 + v^3/3 with v = 1 - u (exact), so E keeps
 // full relative precision where the hardware log would lose it.
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                                                    const float* __restrict__ packed, int n_actions, int n_otiles,
                                                    uint32_t seed_lo, uint32_t seed_hi, uint32_t step, int greedy,
                                                    int32_t* act_out, float* logp_out, float* value_out,
-                                                   float* logits_out) {
+                                                   float* logits_out, uint8_t* records_out) {
     __shared__ uint8_t srec[32 * 64];
     const float *hdrf, *w1f, *b1p, *w2f, *b2p;
     views(packed, T, n_otiles, hdrf, w1f, b1p, w2f, b2p);
@@ -146,8 +149,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const int gr = row0 + r < n ? row0 + r : n - 1;
         const uint4* src = (const uint4*)(recs + (size_t)gr * 64 + off);
         uint4* dst = (uint4*)(srec + r * 64 + off);
-        dst[0] = src[0];
-        dst[1] = src[1];
+        const uint4 v0 = src[0], v1 = src[1];
+        dst[0] = v0;
+        dst[1] = v1;
+        if (records_out && row0 + r < n) {             // the rollout row's copy of the record
+            uint4* o = (uint4*)(records_out + (size_t)(row0 + r) * 64 + off);
+            o[0] = v0;
+            o[1] = v1;
+        }
     }
     __syncthreads();
     const int j = l & 31, h = l >> 5;
@@ -245,20 +254,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             tm = fmaxf(tm, z[r]);
         }
         const float mn = fmaxf(m, tm);
-        if (mn == -INFINITY) continue;                 // nothing of this lane's row so far
-        float acc = 0.0f;
-        #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int a = 32 * o + hid(r, h);
-            acc += fast_exp(z[r] - mn);
-            const float key = greedy ? z[r] : z[r] + gumbel(mix32(rowkey ^ ((uint32_t)a * 0xC2B2AE35u)));
-            const bool up_ = key > best;
-            best = up_ ? key : best;
-            besta = up_ ? a : besta;
-            bestz = up_ ? z[r] : bestz;
+        if (mn != -INFINITY) {                         // else nothing of this lane's row so far
+            float acc = 0.0f;
+            #pragma unroll
+            for (int r = 0; r < 16; ++r) acc += fast_exp(z[r] - mn);
+            s = s * fast_exp(m - mn) + acc;
+            m = mn;
         }
-        s = s * fast_exp(m - mn) + acc;
-        m = mn;
+        // A key is z + g with g <= kGumbelMax, so when tm + kGumbelMax < best no
+        // output of this tile can replace the lane's current best: the noise is
+        // skipped (exact — the same keys are never larger).  Past the legal
+        // actions' tile(s) this holds for every lane of a row with legal moves
+        // (masked outputs sit 103 below).
+        if (greedy ? tm > best : !(tm + kGumbelMax < best)) {
+            #pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int a = 32 * o + hid(r, h);
+                const float key = greedy ? z[r] : z[r] + gumbel(mix32(rowkey ^ ((uint32_t)a * 0xC2B2AE35u)));
+                const bool up_ = key > best;
+                best = up_ ? key : best;
+                besta = up_ ? a : besta;
+                bestz = up_ ? z[r] : bestz;
+            }
+        }
     }
     // combine the two lane halves of each row (lanes j and j+32)
     const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(s, 32);
@@ -369,9 +387,9 @@ int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const flo
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }
 
-int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed, int32_t hidden, int32_t n_actions,
-                   uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out, float* value_out,
-                   float* logits_out, void* stream) {
+int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packed, int32_t hidden, int32_t n_actions,
+                       uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out,
+                       float* value_out, float* logits_out, uint8_t* records_out, void* stream) {
     if (bgx_policy_packed_size(hidden, n_actions) < 0 || n < 0 || (n > 0 && (!records_dev || !packed || !act_out)))
         return BGX_EINVAL;
     if (n == 0) return BGX_OK;
@@ -379,13 +397,23 @@ int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed, i
     const dim3 grid((n + 31) / 32), blk(64);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
+#define BGX_ACT(TT) hipLaunchKernelGGL(k_policy_act<TT>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, \
+                                       step, greedy, act_out, logp_out, value_out, logits_out, records_out)
     switch (T) {
-        case 1: hipLaunchKernelGGL(k_policy_act<1>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
-        case 2: hipLaunchKernelGGL(k_policy_act<2>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
-        case 3: hipLaunchKernelGGL(k_policy_act<3>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
-        default: hipLaunchKernelGGL(k_policy_act<4>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, step, greedy, act_out, logp_out, value_out, logits_out); break;
+        case 1: BGX_ACT(1); break;
+        case 2: BGX_ACT(2); break;
+        case 3: BGX_ACT(3); break;
+        default: BGX_ACT(4); break;
     }
+#undef BGX_ACT
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
+}
+
+int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed, int32_t hidden, int32_t n_actions,
+                   uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out, float* value_out,
+                   float* logits_out, void* stream) {
+    return bgx_policy_act_rec(records_dev, n, packed, hidden, n_actions, seed, step, greedy, act_out, logp_out,
+                              value_out, logits_out, nullptr, stream);
 }
 
 }  // extern "C"
