@@ -402,6 +402,9 @@ struct bgx_engine {
     // overflow counters, two 16-byte sets: a Philox step uses set `ovf_parity`
     // (Args::ovf_count) and its k_order_count zeroes the other set for the next
     // step, so the step needs no separate memset launch
+    hipStream_t step_side;      // BGX_STEP_OVERLAP: light launch beside the heavy one
+    hipEvent_t step_ev[2];
+    int step_overlap;
     int32_t* ovf_base;
     int ovf_parity;
     bool ovf_next_zeroed;

@@ -454,6 +454,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     if (e->lds_log < 9 || e->lds_log > 11) e->lds_log = 10;
     const char* sp = getenv("BGX_SPLIT");
     e->split = !(sp && sp[0] == '0');
+    const char* sov = getenv("BGX_STEP_OVERLAP");
+    e->step_overlap = sov ? atoi(sov) : 1;
     const char* mm = getenv("BGX_MEMO_MODE");
     e->memo_mode = mm ? atoi(mm) : 1;
     Args& A = e->a;
@@ -506,6 +508,8 @@ int bgx_engine_destroy(bgx_engine* e) {
                     e->slow_tables, e->search_ws, e->search_pool, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (hipEvent_t ev : e->search_ev) if (ev) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : e->step_ev) if (ev) (void)hipEventDestroy(ev);
+    if (e->step_side) (void)hipStreamDestroy(e->step_side);
     if (e->search_side) (void)hipStreamDestroy(e->search_side);
     delete e;
     return BGX_OK;
@@ -630,10 +634,30 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
         // hardware wave limit, ~5x the resident waves; doubles go to the overflow tiers).
         // Plain stream order -- no cross-stream wait that a serializing tool
         // (profiler) or a shared hardware queue could deadlock.
-        launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
-        if (heavy < A.B)
-            hipLaunchKernelGGL((k_step<0, 8, 0, true>), dim3(A.B - heavy), dim3(64), 0, s, a, actions_dev, obs_dev,
-                               reward_dev, done_dev, info_dev, heavy);
+        if (e->step_overlap && heavy < A.B) {
+            // fork-join on events: the light launch runs on a side stream beside
+            // the heavy one (filling the CUs its tail leaves idle)
+            if (!e->step_side) {
+                CK(hipStreamCreateWithFlags(&e->step_side, hipStreamNonBlocking));
+                for (hipEvent_t& ev : e->step_ev) CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            }
+            CK(hipEventRecord(e->step_ev[0], s));
+            CK(hipStreamWaitEvent(e->step_side, e->step_ev[0], 0));
+            auto light = [&] {
+                hipLaunchKernelGGL((k_step<0, 8, 0, true>), dim3(A.B - heavy), dim3(64), 0, e->step_side, a,
+                                   actions_dev, obs_dev, reward_dev, done_dev, info_dev, heavy);
+            };
+            if (e->step_overlap == 2) light();
+            launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+            if (e->step_overlap != 2) light();
+            CK(hipEventRecord(e->step_ev[1], e->step_side));
+            CK(hipStreamWaitEvent(s, e->step_ev[1], 0));
+        } else {
+            launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+            if (heavy < A.B)
+                hipLaunchKernelGGL((k_step<0, 8, 0, true>), dim3(A.B - heavy), dim3(64), 0, s, a, actions_dev,
+                                   obs_dev, reward_dev, done_dev, info_dev, heavy);
+        }
         if (A.cls) launch_order(e, s);
     }
     CKL();
