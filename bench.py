@@ -370,7 +370,8 @@ def main():
                    "streams_per_gpu": S},
         "roofline": {"kernel": "env step = k_step<0,10,1> (predicted-doubles prefix) then k_step<0,8,0,true> "
                                "(the rest) + k_order_count/scatter + k_movegen_over tiers, one wave per game, "
-                               "all on the caller's stream; HIP events around bgx_step",
+                               "the light launch on the engine's side stream (event fork-join); HIP events around "
+                               "bgx_step on the shard's stream, per shard of games_per_gpu/shards lanes",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/env step",
                      "traffic_source": traffic_src, "algorithmic_bytes_per_step": Bs * bytes_per_lane, "lanes_per_launch": Bs,
