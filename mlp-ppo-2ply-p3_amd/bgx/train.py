@@ -32,6 +32,7 @@ import time
 import torch
 import torch.distributed as dist
 import torch.nn as nn
+import torch.nn.functional as F
 from torch.amp import GradScaler, autocast
 
 import ctypes
@@ -75,6 +76,12 @@ def features_and_masks(records: torch.Tensor, n_actions: int):
     counts = records[:, 60].to(torch.int32) | (records[:, 61].to(torch.int32) << 8)
     legal = torch.arange(n_actions, device=records.device)[None, :] < counts[:, None]
     return feats, legal
+
+
+def _is_policy_mlp(net) -> bool:
+    """The manual fp16 epoch needs exactly relu(fc1) -> {action_head, value_head}."""
+    return (isinstance(net, PolicyNet) and type(net).forward is PolicyNet.forward
+            and all(getattr(net, k).bias is not None for k in ("fc1", "action_head", "value_head")))
 
 
 class _PPOHead(torch.autograd.Function):
@@ -148,6 +155,68 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
     return parts
 
 
+def _wgrad(g: torch.Tensor, x: torch.Tensor, splits: int = 64) -> torch.Tensor:
+    """g^T x (fp16 [m, N], [m, K]) -> fp32 [N, K]: the weight gradient of a
+    linear layer, a K = m reduction.  hipBLASLt runs this shape (m = 2^20,
+    N x K = 512 x 128) at ~70 TFLOP/s; as `splits` batched GEMMs over row slices
+    plus an fp32 sum of the partials it runs 7-10x faster (tools/gemm_probe.py)."""
+    m = g.shape[0]
+    if m % splits or m < 64 * splits:
+        return (g.t() @ x).float()
+    return torch.bmm(g.view(splits, m // splits, -1).transpose(1, 2), x.view(splits, m // splits, -1)).float().sum(0)
+
+
+def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
+    """The fp16-autocast epoch's forward and backward written out (the same
+    fp16 GEMMs, fp32 accumulation): [action_head; value_head] as ONE GEMM
+    padded to 512 outputs (hipBLASLt: 0.35 vs 0.74 ms at 2^20 x 500), the loss
+    head kernel reading the logits / writing their gradient in place (row stride
+    512), ReLU backward on the stored activations, and split-K weight
+    gradients (_wgrad).  Gradients land in p.grad as fp32, as autograd's would."""
+    eps, c_v, c_e, gscale = coefs
+    W1, b1 = net.fc1.weight, net.fc1.bias
+    Wa, ba = net.action_head.weight, net.action_head.bias
+    wv, bv = net.value_head.weight, net.value_head.bias
+    A, Hd = Wa.shape
+    Ap = (A + 1 + 31) // 32 * 32
+    dev = W1.device
+    with torch.no_grad():
+        W1h, b1h = W1.half(), b1.half()
+        W2h = torch.zeros(Ap, Hd, dtype=torch.float16, device=dev)
+        b2h = torch.zeros(Ap, dtype=torch.float16, device=dev)
+        W2h[:A] = Wa.half(); W2h[A] = wv[0].half()
+        b2h[:A] = ba.half(); b2h[A] = bv[0].half()
+        gW1 = torch.zeros_like(W1); gb1 = torch.zeros_like(b1)
+        gW2 = torch.zeros(Ap, Hd, dtype=torch.float32, device=dev)
+        gb2 = torch.zeros(Ap, dtype=torch.float32, device=dev)
+        L = _lib.load()
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for feats, legal, actions, old_logp, returns, adv, records in chunks:
+            x = feats.half()
+            h = torch.relu(F.linear(x, W1h, b1h))
+            y = F.linear(h, W2h, b2h)                      # [m, Ap]: logits | value | 0
+            m = y.shape[0]
+            vals = y[:, A].contiguous()
+            dy = torch.empty_like(y)
+            dy[:, A + 1:].zero_()
+            dval = torch.empty_like(vals)
+            check(L.bgx_ppo_head(p(y), 1, Ap, p(vals), p(records.contiguous()),
+                                 p(actions.to(torch.int32).contiguous()), p(old_logp.float().contiguous()),
+                                 p(returns.float().contiguous()), p(adv.float().contiguous()), m, A, eps, c_v, c_e,
+                                 gscale, p(dy), Ap, p(dval), p(sums), stream), "bgx_ppo_head")
+            dy[:, A] = dval
+            gW2 += _wgrad(dy, h)
+            gb2 += dy.sum(0, dtype=torch.float32)
+            dh = dy @ W2h
+            dh.masked_fill_(h <= 0, 0)                     # relu backward (grad where out > 0)
+            gW1 += _wgrad(dh, x)
+            gb1 += dh.sum(0, dtype=torch.float32)
+    W1.grad, b1.grad = gW1, gb1
+    Wa.grad, ba.grad = gW2[:A].contiguous(), gb2[:A].contiguous()
+    wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
+
+
 def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step):
     dev = next(net.parameters()).device
     if scaler.is_enabled():
@@ -157,6 +226,10 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
         scale = 1.0
     sums = torch.zeros(3, dtype=torch.float64, device=dev)
     coefs = (EPS_CLIP, VALUE_LOSS_COEF, float(entropy_coef), float(scale) / n_total)
+    manual = amp and os.environ.get("BGX_PPO_MANUAL", "1") != "0" and _is_policy_mlp(net)
+    if manual:
+        _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums)
+        chunks = ()
     for feats, legal, actions, old_logp, returns, adv, records in chunks:
         with autocast(device_type=dev.type, enabled=amp):
             logits, values = net(feats)
