@@ -31,15 +31,18 @@ BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c3", choices=["c3", "c1"])
     ap.add_argument("--horizon", type=int, default=32,
                     help="also time full PPO iterations (T rollout steps + update); 0 = skip")
-    ap.add_argument("--two-ply-batches", type=int, default=1,
+    ap.add_argument("--two-ply-batches", type=int, default=2,
                     help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
     ap.add_argument("--c2-steps", type=int, default=50,
                     help="C2: timed greedy 1-ply self-play steps at B=4096 (0 = skip)")
+    ap.add_argument("--c2-shards", type=int, default=1,
+                    help="C2: the 4,096 games as S engines on S streams (S=2: +7%% alone, but -45%% after the "
+                         "C3/C4 legs have created their streams: more streams than hardware queues)")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--shards", type=int, default=2,
                     help="the B games of a GPU as S engines of B/S lanes on S streams, so one shard's policy "
@@ -144,32 +147,46 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 2):
             "losses_last": {k: ms[-1][k] for k in ("policy_loss", "value_loss", "entropy", "total_loss")}}
 
 
-def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev):
+def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 2):
     """C2: B games per GPU, greedy 1-ply self-play with the value head
     MLP(198->40->1): every step = V over each lane's legal afterstates (mover's
-    one-hot, as legal_board_features) -> first argmax -> env.step."""
+    one-hot, as legal_board_features) -> first argmax -> env.step.  The B games
+    run as `shards` engines on their own streams: at this batch each launch is
+    bound by its slowest lane, so one shard's search runs beside the other's
+    step."""
     import bgx
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead, one_ply
     torch.manual_seed(2)
     vh = ValueHead(PolicyNet(hidden_size=40).to(dev))
-    eng = bgx.Engine(batch=B, max_moves=500, seed=123 + rank, dice="philox", auto_reset=True, device=dev)
-    eng.reset(want_obs=False)
+    S = shards if B % shards == 0 else 1
+    engs = [bgx.Engine(batch=B // S, max_moves=500, seed=123 + rank + 7919 * k, dice="philox", auto_reset=True,
+                       device=dev) for k in range(S)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    for e in engs:
+        e.reset(want_obs=False)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        for e, st in zip(engs, streams):
+            with torch.cuda.stream(st):
+                best, _ = one_ply(e, vh)
+                e.step(best, want_obs=False, want_info=False)
+
     for _ in range(20):                                # burn-in + warm
-        best, _ = one_ply(eng, vh)
-        eng.step(best, want_obs=False, want_info=False)
+        step()
     torch.cuda.synchronize(dev)
     barrier(ws)
     t0 = time.perf_counter()
     for _ in range(steps):
-        best, _ = one_ply(eng, vh)
-        eng.step(best, want_obs=False, want_info=False)
+        step()
     torch.cuda.synchronize(dev)
     barrier(ws)
     el = max_over_ranks(time.perf_counter() - t0, ws)
-    return {"config": f"C2: B={B} games/GPU, 1-ply greedy self-play, value MLP 198->40->1 (argmax over afterstates)",
+    return {"config": f"C2: B={B} games/GPU as {S} shard(s), 1-ply greedy self-play, value MLP 198->40->1 "
+                      "(argmax over afterstates)",
             "env_steps_per_s": sum_over_ranks(float(B * steps), ws) / el, "ms_per_step": el * 1e3 / steps,
-            "steps": steps}
+            "steps": steps, "shards": S}
 
 
 def two_ply_bench(eng, batches: int, ws: int, dev):
@@ -254,7 +271,7 @@ def main():
     } for _ in range(S)]
     pins = [{k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in b.items()}
             for b in bufs] if args.host_mirror else None
-    copy_streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    copy_streams = [torch.cuda.Stream(dev) for _ in range(S)] if args.host_mirror else None
     counts = [torch.empty(Bs, dtype=torch.int16, device=dev) for _ in range(S)]
     gen = torch.Generator(device=dev).manual_seed(99 + rank)
     ev_pairs = []
@@ -389,7 +406,7 @@ def main():
                 eng2.step(a2, want_obs=False, want_info=False)
         line["two_ply"] = two_ply_bench(eng2, args.two_ply_batches, ws, dev)
     if args.c2_steps > 0:
-        line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev)
+        line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev, args.c2_shards)
     if args.horizon > 0 and args.workload in ("c3", "ppo"):
         line["ppo_iteration"] = ppo_iteration_bench(B, args.horizon, ws, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
