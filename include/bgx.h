@@ -201,6 +201,20 @@ int bgx_ppo_head(const void* logits_dev, int32_t dtype, int64_t ld_logits, const
                  float c_value, float c_entropy, float grad_scale, void* dlogits_dev, int64_t ld_dlogits,
                  void* dvalues_dev, double* sums_dev, void* stream);
 
+/* bgx_ppo_head for a [logits | value | 0 ...] layout (one GEMM for both heads,
+ * row stride ld_dlogits <= 512): with pad_value_col != 0 the kernel also writes
+ * the value gradient into column n_actions of dlogits and zeros up to
+ * ld_dlogits; with colsum != NULL (float[BGX_PPO_COLSUM_BLOCKS][512]) each
+ * workgroup writes the column sums of the gradient it stored (fp16-rounded
+ * when dtype = 1) — the bias gradient, summed over the first dimension by the
+ * caller.  dvalues_dev is written as in bgx_ppo_head. */
+#define BGX_PPO_COLSUM_BLOCKS 2048
+int bgx_ppo_head_ex(const void* logits_dev, int32_t dtype, int64_t ld_logits, const void* values_dev,
+                    const uint8_t* records_dev, const int32_t* actions_dev, const float* old_logp_dev,
+                    const float* returns_dev, const float* adv_dev, int32_t n, int32_t n_actions, float eps_clip,
+                    float c_value, float c_entropy, float grad_scale, void* dlogits_dev, int64_t ld_dlogits,
+                    void* dvalues_dev, double* sums_dev, int32_t pad_value_col, float* colsum_dev, void* stream);
+
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
  * evaluation after it (k_eval, the MFMA kernel). */

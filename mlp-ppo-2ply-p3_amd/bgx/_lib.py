@@ -48,6 +48,9 @@ SIGNATURES = {
     "bgx_two_ply_timings": (ctypes.c_int, [_P, _P]),
     "bgx_ppo_head": (ctypes.c_int, [_P, _I32, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.c_float,
                                     ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, ctypes.c_int64, _P, _P, _P]),
+    "bgx_ppo_head_ex": (ctypes.c_int, [_P, _I32, ctypes.c_int64, _P, _P, _P, _P, _P, _P, _I32, _I32, ctypes.c_float,
+                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, ctypes.c_int64, _P, _P, _I32,
+                                       _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
 }
 

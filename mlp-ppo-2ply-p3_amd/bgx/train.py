@@ -155,6 +155,9 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
     return parts
 
 
+PPO_COLSUM_BLOCKS = 2048       # include/bgx.h BGX_PPO_COLSUM_BLOCKS
+
+
 def _wgrad(g: torch.Tensor, x: torch.Tensor, splits: int = 64) -> torch.Tensor:
     """g^T x (fp16 [m, N], [m, K]) -> fp32 [N, K]: the weight gradient of a
     linear layer, a K = m reduction.  hipBLASLt runs this shape (m = 2^20,
@@ -192,6 +195,7 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
         L = _lib.load()
         p = lambda t: ctypes.c_void_p(t.data_ptr())
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        colsum = torch.empty(PPO_COLSUM_BLOCKS, 512, dtype=torch.float32, device=dev)
         for feats, legal, actions, old_logp, returns, adv, records in chunks:
             x = feats.half()
             h = torch.relu(F.linear(x, W1h, b1h))
@@ -199,15 +203,15 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
             m = y.shape[0]
             vals = y[:, A].contiguous()
             dy = torch.empty_like(y)
-            dy[:, A + 1:].zero_()
             dval = torch.empty_like(vals)
-            check(L.bgx_ppo_head(p(y), 1, Ap, p(vals), p(records.contiguous()),
-                                 p(actions.to(torch.int32).contiguous()), p(old_logp.float().contiguous()),
-                                 p(returns.float().contiguous()), p(adv.float().contiguous()), m, A, eps, c_v, c_e,
-                                 gscale, p(dy), Ap, p(dval), p(sums), stream), "bgx_ppo_head")
-            dy[:, A] = dval
+            # dy = [dlogits | dvalue | 0] written by the kernel, with its column sums
+            check(L.bgx_ppo_head_ex(p(y), 1, Ap, p(vals), p(records.contiguous()),
+                                    p(actions.to(torch.int32).contiguous()), p(old_logp.float().contiguous()),
+                                    p(returns.float().contiguous()), p(adv.float().contiguous()), m, A, eps, c_v,
+                                    c_e, gscale, p(dy), Ap, p(dval), p(sums), 1, p(colsum), stream),
+                  "bgx_ppo_head_ex")
             gW2 += _wgrad(dy, h)
-            gb2 += dy.sum(0, dtype=torch.float32)
+            gb2 += colsum.sum(0)[:Ap]
             dh = dy @ W2h
             dh.masked_fill_(h <= 0, 0)                     # relu backward (grad where out > 0)
             gW1 += _wgrad(dh, x)

@@ -18,6 +18,7 @@
 namespace {
 
 constexpr float kMaskLog = -103.27892990343185f;   // log(1e-45) in fp32 (policy.py MASK_LOG)
+constexpr int kPpoColBlocks = BGX_PPO_COLSUM_BLOCKS;
 
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -69,11 +70,13 @@ __global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, 
                                                   const float* __restrict__ returns, const float* __restrict__ adv,
                                                   int n, int A, float eps_clip, float c_value, float c_entropy,
                                                   float gscale, T* __restrict__ dlogits, int64_t ld_dlogits,
-                                                  T* __restrict__ dvalues, double* __restrict__ sums, int vec) {
+                                                  T* __restrict__ dvalues, double* __restrict__ sums, int vec,
+                                                  int pad, float* __restrict__ colsum) {
     const int l = threadIdx.x & 63;
     const int nw = gridDim.x * (blockDim.x >> 6);
     const int j0 = 8 * l;                      // this lane's columns j0 .. j0+7
     double s_pol = 0.0, s_val = 0.0, s_ent = 0.0;
+    float cs[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};   // column sums of the stored gradient
     for (int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < n; row += nw) {
         const T* lg = logits + (int64_t)row * ld_logits;
         const uint8_t* rec = records + (int64_t)row * 64;
@@ -127,16 +130,28 @@ __global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, 
             const float pi = e[i];
             g[i] = gscale * (g_lp * ((j0 + i == act ? 1.0f : 0.0f) - pi) + c_entropy * pi * (lp[i] + ent));
         }
+        const float v = (float)values[row], dv = v - returns[row];
+        const float gv = gscale * c_value * 2.0f * dv;
         T* dl = dlogits + (int64_t)row * ld_dlogits;
         if (vec && j0 + 8 <= A) {
             Vec8<T>::store(dl + j0, g);
-        } else {
             #pragma unroll
-            for (int i = 0; i < 8; ++i) if (j0 + i < A) dl[j0 + i] = (T)g[i];
+            for (int i = 0; i < 8; ++i) cs[i] += (float)(T)g[i];
+        } else {
+            // the row's tail; with `pad` also column A = the value gradient and
+            // zeros up to ld_dlogits (the layout of a [logits | value | 0] GEMM)
+            #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int j = j0 + i;
+                const T t = j < A ? (T)g[i] : (j == A ? (T)gv : (T)0.0f);
+                if (j < A || (pad && j < ld_dlogits)) {
+                    dl[j] = t;
+                    cs[i] += (float)t;
+                }
+            }
         }
         if (l == 0) {
-            const float v = (float)values[row], dv = v - returns[row];
-            dvalues[row] = (T)(gscale * c_value * 2.0f * dv);
+            dvalues[row] = (T)gv;
             s_pol += pol;
             s_val += (double)dv * dv;
             s_ent += ent;
@@ -153,37 +168,62 @@ __global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, 
         for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i][threadIdx.x];
         atomicAdd(sums + threadIdx.x, t);
     }
+    if (colsum) {                              // this workgroup's column sums -> colsum[block][512]
+        __shared__ float cred[4][512];
+        #pragma unroll
+        for (int i = 0; i < 8; ++i) cred[w][j0 + i] = cs[i];
+        __syncthreads();
+        for (int c = threadIdx.x; c < 512; c += blockDim.x) {
+            float t = 0.0f;
+            for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += cred[i][c];
+            colsum[(int64_t)blockIdx.x * 512 + c] = t;
+        }
+    }
 }
 
 }  // namespace
 
 extern int bgx_internal_fail(hipError_t e);
 
-extern "C" int bgx_ppo_head(const void* logits, int32_t dtype, int64_t ld_logits, const void* values,
-                            const uint8_t* records, const int32_t* actions, const float* old_logp,
-                            const float* returns, const float* adv, int32_t n, int32_t n_actions, float eps_clip,
-                            float c_value, float c_entropy, float grad_scale, void* dlogits, int64_t ld_dlogits,
-                            void* dvalues, double* sums, void* stream) {
+extern "C" int bgx_ppo_head_ex(const void* logits, int32_t dtype, int64_t ld_logits, const void* values,
+                               const uint8_t* records, const int32_t* actions, const float* old_logp,
+                               const float* returns, const float* adv, int32_t n, int32_t n_actions, float eps_clip,
+                               float c_value, float c_entropy, float grad_scale, void* dlogits, int64_t ld_dlogits,
+                               void* dvalues, double* sums, int32_t pad_value_col, float* colsum, void* stream) {
     if (n < 0 || n_actions <= 0 || n_actions > 512 || (dtype != 0 && dtype != 1)) return BGX_EINVAL;
+    if (pad_value_col && (ld_dlogits <= n_actions || ld_dlogits > 512)) return BGX_EINVAL;
     if (n > 0 && (!logits || !values || !records || !actions || !old_logp || !returns || !adv || !dlogits ||
                   !dvalues || !sums))
         return BGX_EINVAL;
-    if (n == 0) return BGX_OK;
-    const int blocks = (n + 3) / 4 < 2048 ? (n + 3) / 4 : 2048;
+    if (n == 0 && !colsum) return BGX_OK;
+    // with column sums the grid is fixed (colsum is [kPpoColBlocks][512], every block writes its row)
+    const int blocks = colsum ? kPpoColBlocks : ((n + 3) / 4 < 2048 ? (n + 3) / 4 : 2048);
     hipStream_t s = (hipStream_t)stream;
     const int esz = dtype == 0 ? 4 : 2;
     const int al = dtype == 0 ? 16 : 8;
     const int vec = ((uintptr_t)logits % al == 0 && (uintptr_t)dlogits % al == 0 && (ld_logits * esz) % al == 0 &&
                      (ld_dlogits * esz) % al == 0) ? 1 : 0;
+    const int pad = pad_value_col ? 1 : 0;
     if (dtype == 0)
         hipLaunchKernelGGL(k_ppo_head<float>, dim3(blocks), dim3(256), 0, s, (const float*)logits, ld_logits,
                            (const float*)values, records, actions, old_logp, returns, adv, n, n_actions, eps_clip,
-                           c_value, c_entropy, grad_scale, (float*)dlogits, ld_dlogits, (float*)dvalues, sums, vec);
+                           c_value, c_entropy, grad_scale, (float*)dlogits, ld_dlogits, (float*)dvalues, sums, vec,
+                           pad, colsum);
     else
         hipLaunchKernelGGL(k_ppo_head<_Float16>, dim3(blocks), dim3(256), 0, s, (const _Float16*)logits, ld_logits,
                            (const _Float16*)values, records, actions, old_logp, returns, adv, n, n_actions,
                            eps_clip, c_value, c_entropy, grad_scale, (_Float16*)dlogits, ld_dlogits,
-                           (_Float16*)dvalues, sums, vec);
+                           (_Float16*)dvalues, sums, vec, pad, colsum);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
+extern "C" int bgx_ppo_head(const void* logits, int32_t dtype, int64_t ld_logits, const void* values,
+                            const uint8_t* records, const int32_t* actions, const float* old_logp,
+                            const float* returns, const float* adv, int32_t n, int32_t n_actions, float eps_clip,
+                            float c_value, float c_entropy, float grad_scale, void* dlogits, int64_t ld_dlogits,
+                            void* dvalues, double* sums, void* stream) {
+    return bgx_ppo_head_ex(logits, dtype, ld_logits, values, records, actions, old_logp, returns, adv, n, n_actions,
+                           eps_clip, c_value, c_entropy, grad_scale, dlogits, ld_dlogits, dvalues, sums, 0, nullptr,
+                           stream);
 }
