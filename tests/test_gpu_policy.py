@@ -141,3 +141,36 @@ def test_policy_sampling_no_legal_moves(bgx):
     assert chi2 < dof + 6 * np.sqrt(2 * dof) + 10, (chi2, dof)
     c1 = int(rec[1, 60]) | (int(rec[1, 61]) << 8)
     assert c1 > 0 and torch.all(a[1::2] < c1)
+
+
+def test_rollout_path_in_place(bgx):
+    """The rollout path (PPOTrainer, bench C3): act(engine, out=, records_out=)
+    reads the lane records in place and stores them; step(out=) writes rewards /
+    dones into caller rows.  Same actions, log-probs, values, stored records,
+    rewards, dones and final boards as the copying path, over 40 steps (Philox
+    split dispatch with its side stream, double-buffered overflow counters);
+    B = 3,000 leaves a ragged last 32-row wave in the policy kernel."""
+    from bgx.policy import PolicyNet
+    torch.manual_seed(5)
+    net = PolicyNet(hidden_size=128).cuda()
+    B = 3000
+    e1 = bgx.Engine(batch=B, dice="philox", seed=21)
+    e2 = bgx.Engine(batch=B, dice="philox", seed=21)
+    e1.reset(want_obs=False)
+    e2.reset(want_obs=False)
+    kw = dict(device="cuda")
+    rec_out = torch.empty(B, 64, dtype=torch.uint8, **kw)
+    a2 = torch.empty(B, dtype=torch.int32, **kw)
+    lp2, v2, r2 = (torch.empty(B, **kw) for _ in range(3))
+    d2 = torch.empty(B, dtype=torch.uint8, **kw)
+    for t in range(40):
+        rec = e1.records()
+        a1, lp1, v1 = net.act(rec, seed=9, step=t)
+        net.act(e2, seed=9, step=t, out=(a2, lp2, v2), records_out=rec_out)
+        assert torch.equal(rec, rec_out)
+        assert torch.equal(a1, a2) and torch.equal(lp1, lp2) and torch.equal(v1, v2)
+        _, r1, d1, _ = e1.step(a1, want_obs=False, want_info=False)
+        e2.step(a2, want_obs=False, want_info=False, out=(r2, d2))
+        assert torch.equal(r1, r2) and torch.equal(d1, d2)
+    assert torch.equal(e1.records(), e2.records())
+    assert e1.error() == 0 and e2.error() == 0
