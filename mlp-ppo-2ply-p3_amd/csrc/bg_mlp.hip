@@ -15,7 +15,8 @@
 // f32-MFMA rate).  Every operand x is split x = hi + lo (hi = f16(x),
 // lo = f16(x - hi)) and a product is hi*hi + hi*lo + lo*hi: 22 significant bits
 // per operand, products exact in the f32 accumulator, the dropped lo*lo term
-// below 2^-22 relative.  Power-of-two scales keep the parts in f16's normal
+// below 2^-22 relative.  GEMM1's features are exact f16 values (K order
+// permuted, kperm_src), so only W1 is split: 2 MFMAs per k-block and tile.  Power-of-two scales keep the parts in f16's normal
 // range: per weight matrix (pack time, max |w| -> [2^13, 2^14)) and per wave for
 // the hidden layer; they are undone exactly.  Logits/values match torch fp32 to
 // ~1e-6 (tests/test_gpu_policy.py asserts 1e-5).
@@ -33,27 +34,52 @@ constexpr int kKB1 = (kIn + 15) / 16;     // 13 k-blocks of 16 (features padded 
 constexpr float kMaskLog = -103.27892990343185f;  // log(fp32(1e-45)) (ppo_agent.py:166)
 constexpr int kHdr = 16;                  // header floats: [0] = e1, [1] = e2 (int bits)
 
-__constant__ float kOff15m[16] = {
-    0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
-    6.0f / 15.0f, 7.0f / 15.0f, 8.0f / 15.0f, 9.0f / 15.0f, 10.0f / 15.0f, 11.0f / 15.0f,
-    12.0f / 15.0f, 13.0f / 15.0f, 14.0f / 15.0f, 15.0f / 15.0f};
-
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-// feature k (0..197; 0 beyond) of the row whose 64-byte record starts at rec (LDS)
-__device__ __forceinline__ float feat(const uint8_t* rec, int k) {
-    if (k >= kIn) return 0.0f;
-    if (k >= 196) return (k == 196) == (rec[52] == 0) ? 1.0f : 0.0f;
-    const int p = k >= 98 ? 1 : 0;
-    const int g = k - 98 * p;
-    if (g < 96) {
-        const int n = rec[p * 24 + (g >> 2)];
-        const int u = g & 3;
-        if (u < 3) return n > u ? 1.0f : 0.0f;
-        return n >= 3 ? (float)(n - 3) * 0.5f : 0.0f;
+// GEMM1's K order is permuted so that every feature is an exact f16 value
+// generated without branches (bgx_policy_pack packs W1's columns to match):
+// k-blocks 0-5 = P1 points 0..23, 6-11 = P2 points, 4 features per point
+// [n>=1, n>=2, n>=3, (n-3)/2] — lane half h of k-block kb holds points
+// 4(kb mod 6) + 2h + {0, 1}; k-block 12 (h = 0) = P1 bar/2, P1 off, P2 bar/2,
+// P2 off, one-hot[2], then zeros.  The off features are the counts themselves:
+// their W1 columns are pre-divided by 15 (the reference's off/15).
+// Returns the reference feature index (immutable_board.py:171-212) or -1.
+__host__ __device__ inline int kperm_src(int kb, int h, int i) {
+    if (kb < 12) {
+        const int p = kb >= 6 ? 1 : 0;
+        const int pt = 4 * (kb - 6 * p) + 2 * h + (i >> 2);
+        return 98 * p + 4 * pt + (i & 3);
     }
-    if (g == 96) return (float)rec[48 + p] * 0.5f;
-    return kOff15m[rec[50 + p] & 15];
+    if (kb > 12 || h != 0 || i >= 6) return -1;
+    return i < 2 ? 96 + i : 192 + i;             // 96, 97, 194, 195, 196, 197
+}
+
+// the 8 f16 features of lane half h in k-block kb (K order above) of the row
+// whose 64-byte record starts at rec (LDS)
+__device__ __forceinline__ f16x8 feats8(const uint8_t* rec, int kb, int h) {
+    f16x8 f;
+    if (kb < 12) {
+        const int base = (kb >= 6 ? 24 + 4 * (kb - 6) : 4 * kb) + 2 * h;
+        #pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int n = rec[base + q];
+            f[4 * q + 0] = n >= 1 ? (_Float16)1.0f : (_Float16)0.0f;
+            f[4 * q + 1] = n >= 2 ? (_Float16)1.0f : (_Float16)0.0f;
+            f[4 * q + 2] = n >= 3 ? (_Float16)1.0f : (_Float16)0.0f;
+            f[4 * q + 3] = (_Float16)(n >= 3 ? (float)(n - 3) * 0.5f : 0.0f);
+        }
+    } else {
+        const bool on = h == 0;
+        f[0] = on ? (_Float16)((float)rec[48] * 0.5f) : (_Float16)0.0f;
+        f[1] = on ? (_Float16)(float)rec[50] : (_Float16)0.0f;
+        f[2] = on ? (_Float16)((float)rec[49] * 0.5f) : (_Float16)0.0f;
+        f[3] = on ? (_Float16)(float)rec[51] : (_Float16)0.0f;
+        f[4] = on && rec[52] == 0 ? (_Float16)1.0f : (_Float16)0.0f;
+        f[5] = on && rec[52] != 0 ? (_Float16)1.0f : (_Float16)0.0f;
+        f[6] = (_Float16)0.0f;
+        f[7] = (_Float16)0.0f;
+    }
+    return f;
 }
 
 __device__ __forceinline__ void split(float x, _Float16& hi, _Float16& lo) {
@@ -99,7 +125,8 @@ __device__ __forceinline__ float gumbel(uint32_t w) {
 
 // Packed layout (bgx_policy_pack), in floats:
 //   hdr  [16]                       e1, e2 (int bits)
-//   w1q  [13][T][2][64] x uint4     lane l: W1s[32t + (l&31)][16kb + 8(l>>5) + i], i = 0..7, part 0 = hi, 1 = lo
+//   w1q  [13][T][2][64] x uint4     lane l: W1s[32t + (l&31)][kperm_src(kb, l>>5, i)], i = 0..7, part 0 = hi,
+//                                   1 = lo (off columns / 15; 0 where kperm_src < 0)
 //   b1p  [T][16][64] f32            b1[32t + hid(r, l>>5)] * 2^e1
 //   w2q  [OT][T][2][2][64] x uint4  lane l, sub-block m: W2s[32o + (l&31)][32t + hid(8m + i, l>>5)]
 //   b2p  [OT][16][64] f32           b2[32o + hid(r, l>>5)]  (unscaled)
@@ -170,20 +197,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         #pragma unroll
         for (int r = 0; r < 16; ++r) x1[t][r] = b1p[(t * 16 + r) * 64 + l];
     for (int kb = 0; kb < kKB1; ++kb) {
-        f16x8 bh, bl;
-        #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            _Float16 a, b;
-            split(feat(myrec, 16 * kb + 8 * h + i), a, b);
-            bh[i] = a; bl[i] = b;
-        }
+        const f16x8 bf = feats8(myrec, kb, h);         // exact in f16: no lo part
         #pragma unroll
         for (int t = 0; t < T; ++t) {
             const f16x8 ah = as_h8(w1q[((kb * T + t) * 2 + 0) * 64 + l]);
             const f16x8 al = as_h8(w1q[((kb * T + t) * 2 + 1) * 64 + l]);
-            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, x1[t], 0, 0, 0);
-            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, x1[t], 0, 0, 0);
-            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, x1[t], 0, 0, 0);
+            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, x1[t], 0, 0, 0);
+            x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bf, x1[t], 0, 0, 0);
         }
     }
     // ReLU, then a per-wave scale 2^ex for the split of the hidden layer
@@ -337,8 +357,9 @@ __global__ void k_policy_pack(const float* W1, const float* b1, const float* Wa,
     auto B2 = [&](int o) -> float { return o < A ? ba[o] : (o == A ? bv[0] : 0.0f); };
     if (tid < n1) {
         const int i = tid % 8, l = (tid / 8) % 64, t = (tid / 512) % T, kb = tid / (512 * T);
-        const int hrow = 32 * t + (l & 31), k = 16 * kb + 8 * (l >> 5) + i;
-        const float w = hrow < H && k < kIn ? ldexpf(W1[(size_t)hrow * kIn + k], e1) : 0.0f;
+        const int hrow = 32 * t + (l & 31), k = kperm_src(kb, l >> 5, i);
+        const float wk = hrow < H && k >= 0 ? W1[(size_t)hrow * kIn + k] : 0.0f;
+        const float w = ldexpf(k == 97 || k == 195 ? wk / 15.0f : wk, e1);   // off columns: W / 15
         _Float16 a, b;
         split(w, a, b);
         w1h[(((kb * T + t) * 2 + 0) * 64 + l) * 8 + i] = a;
