@@ -156,12 +156,16 @@ __host__ __device__ inline void views(P base, int T, int OT, P& hdr, P& w1q, P& 
     b2p = w2q + sz_w2q(T, OT);
 }
 
-template <int T>
+// MODE 0: sampling without the logits output (the rollout: no per-output
+// branches in the tile loop); MODE -1: greedy / logits_out as passed
+template <int T, int MODE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_policy_act(const uint8_t* __restrict__ recs, int n,
                                                    const float* __restrict__ packed, int n_actions, int n_otiles,
-                                                   uint32_t seed_lo, uint32_t seed_hi, uint32_t step, int greedy,
+                                                   uint32_t seed_lo, uint32_t seed_hi, uint32_t step, int greedy_arg,
                                                    int32_t* act_out, float* logp_out, float* value_out,
-                                                   float* logits_out, uint8_t* records_out) {
+                                                   float* logits_arg, uint8_t* records_out) {
+    const bool greedy = MODE < 0 ? greedy_arg != 0 : false;
+    float* const logits_out = MODE < 0 ? logits_arg : nullptr;
     __shared__ uint8_t srec[32 * 64];
     const float *hdrf, *w1f, *b1p, *w2f, *b2p;
     views(packed, T, n_otiles, hdrf, w1f, b1p, w2f, b2p);
@@ -418,8 +422,16 @@ int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packe
     const dim3 grid((n + 31) / 32), blk(64);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
-#define BGX_ACT(TT) hipLaunchKernelGGL(k_policy_act<TT>, grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, hi, \
-                                       step, greedy, act_out, logp_out, value_out, logits_out, records_out)
+    const bool plain = !greedy && !logits_out;
+#define BGX_ACT(TT)                                                                                           \
+    do {                                                                                                      \
+        if (plain)                                                                                            \
+            hipLaunchKernelGGL((k_policy_act<TT, 0>), grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, \
+                               hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out);      \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_policy_act<TT, -1>), grid, blk, 0, s, records_dev, n, packed, n_actions, OT,   \
+                               lo, hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out);  \
+    } while (0)
     switch (T) {
         case 1: BGX_ACT(1); break;
         case 2: BGX_ACT(2); break;
