@@ -18,7 +18,7 @@ import torch
 
 from .engine import Engine
 from .types import (ImmutableBoard, Player, decode_move, tensor_from52, board_to_string,  # noqa: F401
-                    FullMove)
+                    render_board, FullMove)
 
 REWARD_INVALID_ACTION = -1.0     # backgammon_env.py:23-28
 REWARD_PASS = 0.0
@@ -188,13 +188,11 @@ class BackgammonEnv(_LaneView):
         return bool((t[opp, lo:lo + 6] > 0).any()) or int(t[2, opp]) > 0
 
     def render(self, mode="human"):
-        """A working text render (the reference's crashes: SURVEY.md §4)."""
+        """backgammon_env.py:253-355's board drawing, with the bar / off lookup
+        that raises IndexError in the reference fixed (types.render_board)."""
         if mode != "human":
             raise NotImplementedError("Only 'human' mode is supported")
-        t = self.board.tensor.cpu()
-        print(board_to_string(self.board))
-        print(f"bar: P1={int(t[2, 0])} P2={int(t[2, 1])}  off: P1={int(t[3, 0])} P2={int(t[3, 1])}  "
-              f"to move: {self.current_player.name}  roll: {self.roll_result}")
+        print(render_board(self.board), end="")
 
     def close(self):
         pass

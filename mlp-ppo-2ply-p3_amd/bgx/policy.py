@@ -80,6 +80,14 @@ class PolicyNet(nn.Module):
             packed = self.pack()
         H, A = self.fc1.out_features, self.action_head.out_features
         if isinstance(records, torch.Tensor):
+            # the kernel reads 64 bytes per row with 16-byte loads: anything else would read
+            # past the allocation or decode garbage
+            if (records.dtype not in (torch.uint8, torch.int8) or records.dim() != 2 or records.shape[1] != 64
+                    or records.device.type != "cuda"):
+                raise ValueError(f"act: records must be a uint8/int8 [n, 64] tensor on the GPU, got "
+                                 f"{records.dtype} {tuple(records.shape)} on {records.device}")
+            if records.device != packed.device:
+                raise ValueError("act: records and the packed weights are on different devices")
             r = records.contiguous()
             rptr, n, dev = r.data_ptr(), r.shape[0], r.device
         else:                                              # a bgx.Engine: lane records in place

@@ -68,8 +68,11 @@ def global_normalize(returns: torch.Tensor, group=None) -> torch.Tensor:
     ws = _world(group)
     if ws == 1:
         return (returns - returns.mean()) / (returns.std() + 1e-5)
-    s = torch.stack([returns.sum(), (returns.double() ** 2).sum().float(),
-                     torch.tensor(float(returns.numel()), device=returns.device)]).double()
+    # all three partial sums in fp64: var = (S2 - n mean^2) / (n - 1) cancels, and a
+    # rank holds millions of returns
+    r64 = returns.double()
+    s = torch.stack([r64.sum(), (r64 * r64).sum(),
+                     torch.tensor(float(returns.numel()), dtype=torch.float64, device=returns.device)])
     dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
     n = s[2]
     mean = s[0] / n

@@ -34,6 +34,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 from torch.amp import GradScaler, autocast
+from torch.distributions import Categorical
 
 import ctypes
 
@@ -136,14 +137,16 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
         with autocast(device_type=dev_type, enabled=amp):
             logits, values = net(feats)
             masked = torch.where(legal, logits.float(), logits.float() + MASK_LOG)
-            logp_all = torch.log_softmax(masked, dim=-1)
-            new_logp = logp_all.gather(1, actions.long()[:, None]).squeeze(1)
+            # torch.distributions.Categorical(probs) as ppo_agent.py:273-291: log_prob and
+            # entropy on log(clamp(probs, eps, 1 - eps))
+            dist_ = Categorical(torch.softmax(masked, dim=-1))
+            new_logp = dist_.log_prob(actions.long())
             ratios = torch.exp(new_logp - old_logp)
             surr1 = ratios * adv
             surr2 = torch.clamp(ratios, 1 - EPS_CLIP, 1 + EPS_CLIP) * adv
             policy_loss = -torch.min(surr1, surr2).mean()
             value_loss = nn.functional.mse_loss(values.float().squeeze(-1), returns)
-            entropy = -(logp_all.exp() * logp_all).sum(-1).mean()
+            entropy = dist_.entropy().mean()
             loss = policy_loss + VALUE_LOSS_COEF * value_loss - entropy_coef * entropy
         scaler.scale(loss * w).backward()
         parts += torch.tensor([policy_loss.item(), value_loss.item(), entropy.item(), loss.item()],
@@ -162,11 +165,21 @@ def _wgrad(g: torch.Tensor, x: torch.Tensor, splits: int = 64) -> torch.Tensor:
     """g^T x (fp16 [m, N], [m, K]) -> fp32 [N, K]: the weight gradient of a
     linear layer, a K = m reduction.  hipBLASLt runs this shape (m = 2^20,
     N x K = 512 x 128) at ~70 TFLOP/s; as `splits` batched GEMMs over row slices
-    plus an fp32 sum of the partials it runs 7-10x faster (tools/gemm_probe.py)."""
+    (fp32 partials: no fp16 overflow however many rows a slice sums) plus an
+    fp32 sum of the partials it runs 7-10x faster (tools/gemm_probe.py)."""
     m = g.shape[0]
     if m % splits or m < 64 * splits:
-        return (g.t() @ x).float()
-    return torch.bmm(g.view(splits, m // splits, -1).transpose(1, 2), x.view(splits, m // splits, -1)).float().sum(0)
+        return torch.mm(g.t(), x, out_dtype=torch.float32)
+    return torch.bmm(g.view(splits, m // splits, -1).transpose(1, 2), x.view(splits, m // splits, -1),
+                     out_dtype=torch.float32).sum(0)
+
+
+# Rows per update of the reference (T_HORIZON x NUM_ENVS, agent/config.py:4-6).  The
+# manual fp16 epoch writes per-row gradients at GradScaler scale / min(n, REF_ROWS):
+# the per-row fp16 magnitudes of the reference's own update, whatever the batch
+# (scale / n at 4M rows would push them into fp16's subnormal range); the remaining
+# factor min(n, REF_ROWS) / n is applied in fp32 to the summed weight gradients.
+REF_ROWS = 4096
 
 
 def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
@@ -176,7 +189,9 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
     head kernel reading the logits / writing their gradient in place (row stride
     512), ReLU backward on the stored activations, and split-K weight
     gradients (_wgrad).  Gradients land in p.grad as fp32, as autograd's would."""
-    eps, c_v, c_e, gscale = coefs
+    eps, c_v, c_e, gscale = coefs              # gscale = GradScaler scale / n_total
+    row_scale = gscale * n_total / min(n_total, REF_ROWS)
+    post = min(n_total, REF_ROWS) / n_total    # fp32 factor back to scale / n_total
     W1, b1 = net.fc1.weight, net.fc1.bias
     Wa, ba = net.action_head.weight, net.action_head.bias
     wv, bv = net.value_head.weight, net.value_head.bias
@@ -208,7 +223,7 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
             check(L.bgx_ppo_head_ex(p(y), 1, Ap, p(vals), p(records.contiguous()),
                                     p(actions.to(torch.int32).contiguous()), p(old_logp.float().contiguous()),
                                     p(returns.float().contiguous()), p(adv.float().contiguous()), m, A, eps, c_v,
-                                    c_e, gscale, p(dy), Ap, p(dval), p(sums), 1, p(colsum), stream),
+                                    c_e, row_scale, p(dy), Ap, p(dval), p(sums), 1, p(colsum), stream),
                   "bgx_ppo_head_ex")
             gW2 += _wgrad(dy, h)
             gb2 += colsum.sum(0)[:Ap]
@@ -216,6 +231,9 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
             dh.masked_fill_(h <= 0, 0)                     # relu backward (grad where out > 0)
             gW1 += _wgrad(dh, x)
             gb1 += dh.sum(0, dtype=torch.float32)
+        if post != 1.0:
+            for t in (gW1, gb1, gW2, gb2):
+                t.mul_(post)
     W1.grad, b1.grad = gW1, gb1
     Wa.grad, ba.grad = gW2[:A].contiguous(), gb2[:A].contiguous()
     wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
@@ -253,7 +271,7 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
 class PPOTrainer:
     def __init__(self, batch: int = 65536, horizon: int = 64, hidden: int = 128, n_actions: int = 500,
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
-                 chunk: int = 1 << 20, fused: bool | None = None):
+                 chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True):
         self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.group = process_group
         self.rank = dist.get_rank(process_group) if _world(process_group) > 1 else 0
@@ -261,6 +279,7 @@ class PPOTrainer:
         self.returns_mode = returns
         self.chunk = chunk
         self.fused = (self.dev.type == "cuda") if fused is None else fused
+        self.amp = amp            # the reference's autocast (fp16 on the GPU); False = fp32 update
         self.eng = Engine(batch=batch, max_moves=n_actions, seed=seed * 1_000_003 + self.rank, dice="philox",
                           auto_reset=True, device=self.dev)
         torch.manual_seed(seed)
@@ -312,6 +331,17 @@ class PPOTrainer:
         self.total_episodes += eps
         return eps
 
+    def load_rollout(self, records, actions, logp, values, rewards, dones):
+        """Fill the [T, B] rollout buffers from given data (e.g. a reference
+        agent's memory, step-major) instead of running rollout()."""
+        src = {"records": records, "actions": actions, "logp": logp, "values": values, "rewards": rewards,
+               "dones": dones}
+        for k, v in src.items():
+            v = torch.as_tensor(v)
+            if v.numel() != self.buf[k].numel():
+                raise ValueError(f"load_rollout: {k} has {v.numel()} elements, the buffer {self.buf[k].numel()}")
+            self.buf[k].copy_(v.reshape(self.buf[k].shape).to(self.buf[k].dtype))
+
     def update(self):
         """ppo_agent.py:218-366 on the device buffers."""
         buf = self.buf
@@ -339,7 +369,7 @@ class PPOTrainer:
         parts = torch.zeros(4, dtype=torch.float64)
         for _ in range(NUM_EPOCHS):
             parts += ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
-                               fused=self.fused)
+                               amp=self.amp, fused=self.fused)
         progress = min(1.0, self.total_episodes / ENTROPY_ANNEAL_EPISODES)       # ppo_agent.py:193-197
         self.entropy_coef = ENTROPY_COEF_START - progress * (ENTROPY_COEF_START - ENTROPY_COEF_END)
         p = (parts / NUM_EPOCHS).tolist()

@@ -167,6 +167,45 @@ def board_to_string(board: ImmutableBoard) -> str:          # immutable_board.py
     return "\n".join(lines)
 
 
+_TOKENS = ("●", "○")                                          # backgammon_env.py:15-18
+
+
+def render_board(board: ImmutableBoard) -> str:
+    """The text of BackgammonEnv.render (backgammon_env.py:253-355) with its bar /
+    off lookup fixed: the reference reads tensor[player, BAR=24] on a (4,24)
+    tensor and raises IndexError; here bar = tensor[2, p] and off = tensor[3, p].
+    Returns the printed text (render() prints it)."""
+    t = board.tensor.cpu()
+    out = []
+    cnt, col = [0] * 24, [" "] * 24
+    for i in range(24):
+        a, b = int(t[0, i]), int(t[1, i])
+        if a > 0 and b > 0:
+            out.append(f"Invalid board state at point {i}: Both players have checkers.")
+            col[i] = "?"
+        elif a > 0 or b > 0:
+            cnt[i], col[i] = (a, _TOKENS[0]) if a > 0 else (b, _TOKENS[1])
+
+    def half(points, p):
+        bar, off = int(t[2, p]), int(t[3, p])
+        tok = _TOKENS[p]
+        for lvl in range(max(max(cnt[q] for q in points), bar, off)):
+            cells = [f"{col[q] if cnt[q] > lvl else ' ':^3}" for q in points]
+            mid = f"{tok if bar > lvl else ' ':^3}"
+            end = f"{tok if off > lvl else ' ':^3}"
+            out.append("|  " + " | ".join(cells[:6]) + f" | {mid} | " + " | ".join(cells[6:]) + f" | {end} |")
+
+    rule = "|------------------------------------|     |-----------------------------------|     |"
+    out.append("| 12 | 13 | 14 | 15 | 16 | 17 | BAR | 18 | 19 | 20 | 21 | 22 | 23 | OFF |")
+    out.append(f"|------------Outer Board-------------|     |-----------P={_TOKENS[1]} Home Board----------|     |")
+    half(list(range(12, 24)), 1)
+    out.append(rule)
+    half(list(range(11, -1, -1)), 0)
+    out.append(f"|------------Outer Board-------------|     |-----------P={_TOKENS[0]} Home Board----------|     |")
+    out.append("| 11 | 10 | 9  | 8  | 7  | 6  | BAR | 5  | 4  | 3  | 2  | 1  | 0  | OFF |\n")
+    return "\n".join(out) + "\n"
+
+
 def get_all_possible_moves(player: Player, board: ImmutableBoard, roll_result) -> List[FullMove]:
     """moves/get_all_moves.py:9-70 on the HIP move generator (complete list, no truncation)."""
     e = util_engine(1)

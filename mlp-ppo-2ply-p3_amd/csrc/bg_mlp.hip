@@ -315,7 +315,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const float v_fin = h == 0 ? value + value2 : 0.0f;   // the value row sits in exactly one half
     if (h == 0 && grow < n) {
         act_out[grow] = a_fin;
-        if (logp_out) logp_out[grow] = z_fin - (mm + logf(ss));
+        // Categorical.log_prob = log(clamp(p, eps, 1 - eps)) (torch clamp_probs), in the log domain
+        if (logp_out) logp_out[grow] = fminf(fmaxf(z_fin - (mm + logf(ss)), -15.942384719848633f),
+                                             -1.1920930376163597e-07f);
         if (value_out) value_out[grow] = v_fin;
     }
 }

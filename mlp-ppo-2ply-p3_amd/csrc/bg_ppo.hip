@@ -19,6 +19,9 @@ namespace {
 
 constexpr float kMaskLog = -103.27892990343185f;   // log(1e-45) in fp32 (policy.py MASK_LOG)
 constexpr int kPpoColBlocks = BGX_PPO_COLSUM_BLOCKS;
+// fp32 log(eps) and log(1 - eps), eps = FLT_EPSILON (torch clamp_probs bounds)
+constexpr float kLogEps = -15.942384719848633f;
+constexpr float kLog1mEps = -1.1920930376163597e-07f;
 
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -101,19 +104,30 @@ __global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, 
         for (int i = 0; i < 8; ++i) { e[i] = z[i] == -INFINITY ? 0.0f : __expf(z[i] - m); se += e[i]; }
         se = wave_sum(se);
         const float lse = m + __logf(se), inv = 1.0f / se;
-        float lp[8], ent = 0.0f;
+        // torch.distributions.Categorical(probs) semantics (ppo_agent.py:273-291):
+        // log_prob and entropy use L = log(clamp(p, eps, 1 - eps)) (clamp_probs),
+        // whose gradient is zero outside [eps, 1 - eps]
+        float lp[8], inb[8], ent = 0.0f, s_in = 0.0f;
         #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            lp[i] = z[i] - lse;
+            const float u = z[i] - lse;
+            inb[i] = (u >= kLogEps && u <= kLog1mEps) ? 1.0f : 0.0f;
+            lp[i] = fminf(fmaxf(u, kLogEps), kLog1mEps);
             e[i] *= inv;                           // p
             ent -= z[i] == -INFINITY ? 0.0f : e[i] * lp[i];
+            s_in += e[i] * inb[i];
         }
         ent = wave_sum(ent);
+        s_in = wave_sum(s_in);
         const int act = actions[row];
-        float la = 0.0f;
+        float la = 0.0f, ina = 0.0f;
         #pragma unroll
-        for (int i = 0; i < 8; ++i) la = (act & 7) == i ? lp[i] : la;
-        const float nl = __shfl(la, (act >> 3) & 63);          // log pi(act)
+        for (int i = 0; i < 8; ++i) {
+            la = (act & 7) == i ? lp[i] : la;
+            ina = (act & 7) == i ? inb[i] : ina;
+        }
+        const float nl = __shfl(la, (act >> 3) & 63);          // log pi(act), clamped
+        const float in_a = __shfl(ina, (act >> 3) & 63);
         const float a = adv[row];
         const float r = __expf(nl - old_logp[row]);
         const float s1 = r * a;
@@ -123,12 +137,15 @@ __global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, 
         // d(-min(s1, s2))/d logp: torch min() splits ties, clamp() passes inside [lo, hi]
         const float w1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
         const float w2 = (1.0f - w1) * ((r >= 1.0f - eps_clip && r <= 1.0f + eps_clip) ? 1.0f : 0.0f);
-        const float g_lp = -a * r * (w1 + w2);
+        const float g_lp = -a * r * (w1 + w2) * in_a;
+        // d/dz_k of  -min(.) - c_e * H  with H = -sum L_j p_j:
+        //   g_lp (d_ka - p_k) + c_e p_k (L_k + in_k + H - sum_j p_j in_j)
+        const float ent_c = ent - s_in;
         float g[8];
         #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const float pi = e[i];
-            g[i] = gscale * (g_lp * ((j0 + i == act ? 1.0f : 0.0f) - pi) + c_entropy * pi * (lp[i] + ent));
+            g[i] = gscale * (g_lp * ((j0 + i == act ? 1.0f : 0.0f) - pi) + c_entropy * pi * (lp[i] + inb[i] + ent_c));
         }
         const float v = (float)values[row], dv = v - returns[row];
         const float gv = gscale * c_value * 2.0f * dv;

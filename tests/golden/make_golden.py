@@ -15,6 +15,13 @@ arithmetic.  Output files (all data, no reference source):
   traces.npz     G4  full seeded random-policy game traces (single env)
   mlp.npz        G5  BackgammonPolicyNetwork weights + inputs -> logits/values
   ppo.npz        G6  one select_action + one update() on a fixed batch (CPU)
+  ppo_fp32.npz   G6b the reference update() with autocast disabled (fp32), 1,024 rows
+  ppo_fp16.npz   G6c the reference update() under fp16 autocast + GradScaler (the
+                     reference's CUDA numerics, emulated by CPU fp16 autocast)
+  misc.npz       G7  get_all_dice_rolls_tensor(), board_to_string / render text,
+                     env.legal_moves along seeded single-env games
+
+  python tests/golden/make_golden.py [name ...]   (default: every file)
 """
 from __future__ import annotations
 
@@ -391,7 +398,127 @@ def gen_ppo(feat, mg):
     return out
 
 
+def gen_ppo_batch(mg, mode: str, N=16, T=64):
+    """G6b/G6c: the reference agent's update() on a 1,024-row batch built from
+    G1 positions, autocast switched to fp32 (mode "fp32") or fp16 ("fp16", the
+    dtype CUDA autocast uses).  Rows carry their board + player + legal count
+    (mask = 1 for the first n, all-zero when n == 0, as backgammon_env.py:207-243),
+    so the GPU trainer can rebuild them as 64-byte records."""
+    import src.agent.ppo_agent as pa
+    from torch.amp import autocast as _ac
+    if mode == "fp32":
+        pa.autocast = lambda device_type, **k: _ac(device_type, enabled=False)
+    else:
+        pa.autocast = lambda device_type, **k: _ac(device_type, dtype=torch.float16)
+    rows = np.arange(N * T) * 2 % len(mg["counts"])
+    boards = mg["boards"][rows]
+    players = mg["players"][rows]
+    counts = np.minimum(mg["counts"][rows], 500).astype(np.int32)
+    obs = torch.stack([from52(boards[i]).get_board_features(Player(int(players[i]))) for i in range(N * T)]).float()
+    masks = torch.zeros(N * T, 500)
+    for i, c in enumerate(counts):
+        masks[i, :int(c)] = 1.0
+    torch.manual_seed(21)
+    agent = pa.BackgammonPPOAgent(action_size=500, device=torch.device("cpu"))
+    init_sd = {k: v.clone().numpy() for k, v in agent.policy_network.state_dict().items()}
+    rng = np.random.RandomState(31)
+    rewards = rng.choice([0.0] * 8 + [1.0, -1.0, 1.5, 2.0, -1.5], size=N * T).astype(np.float32)
+    dones = rng.rand(N * T) < 0.1
+    torch.manual_seed(41)
+    actions = []
+    for t in range(T):
+        a = agent.select_action(obs[t * N:(t + 1) * N], masks[t * N:(t + 1) * N])
+        actions.append(a)
+        for i in range(N):
+            agent.memory[-N + i]["reward"] = torch.tensor([rewards[t * N + i]])
+            agent.memory[-N + i]["done"] = torch.tensor([bool(dones[t * N + i])])
+    old_logp = torch.cat([m["action_log_prob"] for m in agent.memory]).detach().numpy()
+    old_v = torch.cat([m["state_value"] for m in agent.memory]).detach().numpy()
+    agent.update()
+    pa.autocast = _ac
+    out = dict(N=N, T=T, boards=boards, players=players, counts=counts, obs=obs.numpy(), rewards=rewards,
+               dones=dones, actions=np.concatenate(actions).astype(np.int64), old_logp=old_logp, old_v=old_v,
+               losses=np.array([agent.last_policy_loss, agent.last_value_loss,
+                                agent.last_entropy_loss, agent.last_total_loss], np.float64),
+               entropy_coef=agent.entropy_coef)
+    for k, v in init_sd.items():
+        out["init_" + k] = v
+    for k, v in agent.policy_network.state_dict().items():
+        out["final_" + k] = v.numpy()
+    print(f"G6 ppo ({mode}): update() on {N * T} rows, losses {out['losses']}")
+    return out
+
+
+class _FixedBarOff:
+    """render() indexes board.tensor[player, BAR=24] / [player, BEAR_OFF=25] on a
+    (4,24) tensor and raises IndexError.  This read-only view maps
+    those two indices to the bar / off channels (tensor[2, p], tensor[3, p]), the
+    evident intent, so the fixed layout can be captured; the reference code runs
+    unmodified."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def __getitem__(self, ix):
+        if isinstance(ix, tuple) and len(ix) == 2 and isinstance(ix[1], int) and ix[1] >= 24:
+            return self.t[2 if ix[1] == 24 else 3, ix[0]]
+        return self.t[ix]
+
+
+def gen_misc(mg):
+    """G7: dice-roll table, board_to_string / render text, env.legal_moves."""
+    import contextlib
+    import io
+    from src.moves.get_all_dice_rolls import get_all_dice_rolls_tensor
+    from src.board.immutable_board import board_to_string
+    rolls, probs = get_all_dice_rolls_tensor()
+    out = dict(rolls=rolls.numpy(), probs=probs.numpy())
+    idx = list(range(0, len(edge_boards()) * 72, 72)) + list(range(1100, 1400, 10))
+    strs, rend = [], []
+    env = BackgammonEnv()
+    for i in idx:
+        b = from52(mg["boards"][i])
+        strs.append(board_to_string(b))
+        env.board = types.SimpleNamespace(tensor=_FixedBarOff(b.tensor))
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            env.render()
+        rend.append(buf.getvalue())
+    out.update(str_idx=np.array(idx, np.int64), board_strings=np.array(strs), render=np.array(rend))
+    # legal_moves along seeded games (single env, random legal policy)
+    lm_seed, lm_step, lm_moves, lm_off = [], [], [], [0]
+    for s in range(6):
+        env = BackgammonEnv()
+        env.seed(100 + s)
+        pol = np.random.RandomState(500 + s)
+        env.reset()
+        for step in range(60):
+            mv = [enc(m) for m in env.legal_moves]
+            lm_seed.append(100 + s)
+            lm_step.append(step)
+            lm_moves.extend(mv)
+            lm_off.append(len(lm_moves))
+            n = len(mv)
+            _, _, done, _ = env.step(int(pol.randint(n)) if n else 0)
+            if done:
+                env.reset()
+    out.update(lm_seed=np.array(lm_seed), lm_step=np.array(lm_step), lm_moves=np.array(lm_moves, np.uint64),
+               lm_off=np.array(lm_off, np.int64))
+    print(f"G7 misc: 21 rolls, {len(idx)} board strings / renders, {len(lm_step)} legal_moves lists")
+    return out
+
+
 def main():
+    want = set(sys.argv[1:])
+    if want:
+        mg = dict(np.load(os.path.join(OUT, "movegen.npz")))
+        if "ppo_fp32" in want:
+            np.savez_compressed(os.path.join(OUT, "ppo_fp32.npz"), **gen_ppo_batch(mg, "fp32"))
+        if "ppo_fp16" in want:
+            np.savez_compressed(os.path.join(OUT, "ppo_fp16.npz"), **gen_ppo_batch(mg, "fp16"))
+        if "misc" in want:
+            np.savez_compressed(os.path.join(OUT, "misc.npz"), **gen_misc(mg))
+        return
     mg = gen_movegen()
     np.savez_compressed(os.path.join(OUT, "movegen.npz"), **mg)
     feat = gen_features(mg)
@@ -402,6 +529,9 @@ def main():
     np.savez_compressed(os.path.join(OUT, "traces.npz"), **tr)
     np.savez_compressed(os.path.join(OUT, "mlp.npz"), **gen_mlp(feat))
     np.savez_compressed(os.path.join(OUT, "ppo.npz"), **gen_ppo(feat, mg))
+    np.savez_compressed(os.path.join(OUT, "ppo_fp32.npz"), **gen_ppo_batch(mg, "fp32"))
+    np.savez_compressed(os.path.join(OUT, "ppo_fp16.npz"), **gen_ppo_batch(mg, "fp16"))
+    np.savez_compressed(os.path.join(OUT, "misc.npz"), **gen_misc(mg))
 
 
 if __name__ == "__main__":

@@ -78,3 +78,30 @@ def test_legal_board_features_and_features(bgx, golden):
     n = int(env.action_mask.sum())
     ref = bgx.generate_all_board_features(env.board, env.current_player, env.legal_moves)
     assert lbf.shape == (500, 198) and torch.equal(lbf[:n], ref) and not lbf[n:].any()
+
+
+def test_env_legal_moves_and_render(bgx, golden, capsys):
+    """env.legal_moves (backgammon_env.py:198-243, FullMove lists in reference
+    order) along seeded games, and render() on the lane's board (golden G7)."""
+    from bgx.types import render_board
+    g = golden("misc")
+    seeds = g["lm_seed"]
+    for s in np.unique(seeds):
+        sel = np.where(seeds == s)[0]
+        env = bgx.BackgammonEnv()
+        env.seed(int(s))
+        pol = np.random.RandomState(500 + int(s) - 100)
+        env.reset()
+        for j in sel:
+            want = g["lm_moves"][g["lm_off"][j]:g["lm_off"][j + 1]]
+            lm = env.legal_moves
+            got = [sum((int(m.start) | (int(m.end) << 5) | (int(bool(m.hits_blot)) << 10) | (1 << 15)) << (16 * i)
+                       for i, m in enumerate(fm.sub_move_commands)) for fm in lm]
+            assert got == [int(v) for v in want], (s, j)
+            assert all(fm.player == env.current_player for fm in lm)
+            n = len(lm)
+            _, _, done, _ = env.step(int(pol.randint(n)) if n else 0)
+            if done:
+                env.reset()
+        env.render()
+        assert capsys.readouterr().out == render_board(env.board)

@@ -177,3 +177,36 @@ def test_two_rank_ppo_epoch_equals_full_batch():
     for i, p in enumerate(net.parameters()):
         assert np.allclose(res[0][i], p.detach().numpy(), atol=1e-5, rtol=1e-4)
         assert np.allclose(res[1][i], res[0][i])
+
+
+def _norm_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=ws)
+    R = _big_returns()
+    n = R.numel() // ws
+    q.put((rank, global_normalize(R[rank * n:(rank + 1) * n]).numpy()))
+    torch.distributed.destroy_process_group()
+
+
+def _big_returns():
+    # discounted-return-like values: mostly small, a long tail toward +-2, offset mean
+    g = torch.Generator().manual_seed(7)
+    return (0.3 + 0.6 * torch.randn(1 << 21, generator=g) * torch.rand(1 << 21, generator=g)).float()
+
+
+def test_two_rank_global_normalize_large():
+    """2^21 returns over 2 ranks (gloo): the fp64 all-reduced (sum, sum of squares, n)
+    normalisation equals the single-process (R - mean) / (std + 1e-5) within 1e-6."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_norm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    R = _big_returns()
+    full = ((R - R.mean()) / (R.std() + 1e-5)).numpy()
+    got = np.concatenate([res[0], res[1]])
+    assert np.abs(got - full).max() < 1e-6
