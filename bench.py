@@ -189,13 +189,13 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
             "steps": steps, "shards": S}
 
 
-def two_ply_bench(eng, batches: int, ws: int, dev):
+def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
     """C4: 2-ply expectimax over the 21 rolls for every lane's current position
-    (B roots per GPU), value head MLP(198->40->1) on MFMA."""
+    (B roots per GPU), value head MLP(198->H->1) on MFMA."""
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead, two_ply, two_ply_timings
     torch.manual_seed(1)
-    vnet = PolicyNet(hidden_size=40).to(dev)
+    vnet = PolicyNet(hidden_size=hidden).to(dev)
     vh = ValueHead(vnet)
     two_ply(eng, vh)                               # warm (workspace sizing, code load)
     torch.cuda.synchronize(dev)
@@ -215,22 +215,26 @@ def two_ply_bench(eng, batches: int, ws: int, dev):
     el = max_over_ranks(time.perf_counter() - t0, ws)
     roots = sum_over_ranks(float(eng.batch * batches), ws)
     leaves_all = sum_over_ranks(float(leaves), ws)
-    flop_per_leaf = 2 * 198 * 40 + 2 * 40
+    flop_per_leaf = 2 * 198 * hidden + 2 * hidden
+    nt = (hidden + 15) // 16
     # k_eval (the MFMA kernel): algorithmic FLOPs of its leaves / its HIP-event time
     eval_tflops = leaves * flop_per_leaf / (eval_ms / batches * 1e-3) / batches / 1e12 if eval_ms > 0 else None
-    return {"config": "C4: B=65536 roots/GPU, 2-ply expectimax over 21 rolls, value MLP 198->40->1 "
-                      "(W1 split hi+lo on f16 MFMA, exact f16 features; fp32-equivalent)",
+    return {"config": f"C4: B={eng.batch} roots/GPU, 2-ply expectimax over 21 rolls, value MLP 198->{hidden}->1 "
+                      "(W1 split hi+lo on f16 MFMA, exact f16 features; fp32-equivalent); leaves encoded with "
+                      "the root mover's one-hot, min over replies",
+            "hidden": hidden, "batches": batches,
             "root_decisions_per_s": roots / el, "leaf_evals_per_s": leaves_all / el,
             "leaves_per_root": leaves_all / roots, "reply_enumerations": jobs * ws, "seconds": el,
             "enumeration_ms_per_batch": enum_ms / batches, "evaluation_ms_per_batch": eval_ms / batches,
-            "roofline": {"kernel": "k_eval: leaf pool -> f16-exact features -> W1 hi+lo on "
+            "roofline": {"kernel": f"k_eval<{nt}>: leaf pool -> f16-exact features -> W1 hi+lo on "
                                    "v_mfma_f32_32x32x16_f16 -> value head -> per-job min (HIP events)",
                          "bound": "mfma", "achieved": eval_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": eval_tflops / BF16_PEAK_TFLOPS if eval_tflops else None,
                          "flop_per_leaf": flop_per_leaf,
-                         "issued_over_algorithmic": 2 * (48 / 40) * (208 / 198),
-                         "note": "issued MFMA work = algorithmic x 2 (W1 hi+lo rows for fp32 accuracy) x 48/40 "
-                                 "(H=40 as three 16-unit hi+lo tiles) x 208/198 (K padding, bias as a feature)"}}
+                         "issued_over_algorithmic": 2 * (16 * nt / hidden) * (208 / 198),
+                         "note": f"issued MFMA work = algorithmic x 2 (W1 hi+lo rows for fp32 accuracy) x "
+                                 f"{16 * nt}/{hidden} (H as {nt} 16-unit hi+lo tiles) x 208/198 (K padding, bias "
+                                 "as a feature)"}}
 
 
 def main():
@@ -405,6 +409,8 @@ def main():
                 a2, _, _ = net.act(eng2, seed=5, step=i)
                 eng2.step(a2, want_obs=False, want_info=False)
         line["two_ply"] = two_ply_bench(eng2, args.two_ply_batches, ws, dev)
+        # the same roots with the reference's H = 128 value head (agent/config.py:8)
+        line["two_ply_h128"] = two_ply_bench(eng2, 1, ws, dev, hidden=128)
     if args.c2_steps > 0:
         line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev, args.c2_shards)
     if args.horizon > 0 and args.workload in ("c3", "ppo"):

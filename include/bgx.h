@@ -162,7 +162,7 @@ int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packe
                        int32_t n_actions, uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out,
                        float* logp_out, float* value_out, float* logits_out, uint8_t* records_out, void* stream);
 
-/* ---- value head search: V(x) = value_head(relu(fc1 x)), H <= 64 ----
+/* ---- value head search: V(x) = value_head(relu(fc1 x)), H <= 128 ----
  * bgx_value_pack packs fc1.weight [H][198], fc1.bias [H], value_head.weight [H],
  * value_head.bias [1] into bgx_value_packed_size(H) floats (MFMA operand order);
  * value_bias is value_head.bias[0] passed by value. */
@@ -177,8 +177,10 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked_dev, int32_t hidden, float v
                 float* bestv_out, float* values_out, void* stream);
 
 /* 2-ply expectimax over the 21 rolls (get_all_dice_rolls.py:5-34) for every lane:
- * Q(a) = sum_r p_r min_{opponent replies b} V(enc(b, opponent)), leaf = a when the
- * opponent cannot move; best_out = first argmax Q.  q_out float[B][max_moves] and
+ * Q(a) = sum_r p_r min_{opponent replies b} V(enc(b, mover)), leaf = a when the
+ * opponent cannot move (every leaf carries the root mover's one-hot, the
+ * reference's evaluate_board(board, current_player), expect_minmax.py:57-58,
+ * 100-143); best_out = first argmax Q.  q_out float[B][max_moves] and
  * bestq_out may be NULL; stats_host (may be NULL) receives {leaves evaluated,
  * (afterstate, roll) jobs, afterstates}.  Synchronises the stream (sizes its
  * workspace from the afterstate count). */

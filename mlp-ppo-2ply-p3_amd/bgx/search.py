@@ -1,7 +1,8 @@
 """1-ply greedy and 2-ply expectimax move selection over engine lanes
 (the reference's intended moves/expect_minmax.py, which is
 commented out there).  V = value_head(relu(fc1 x)) of a
-BackgammonPolicyNetwork (policy_network.py:54-56), H <= 64 (C2/C4 use H = 40).
+BackgammonPolicyNetwork (policy_network.py:54-56), H <= 128 (C2/C4 use H = 40;
+the reference trains H = 128, agent/config.py:8).
 """
 from __future__ import annotations
 
@@ -26,7 +27,7 @@ class ValueHead:
         self.hidden = net.fc1.out_features
         n = L.bgx_value_packed_size(self.hidden)
         if n < 0:
-            raise ValueError(f"value search supports hidden <= 64 (got {self.hidden})")
+            raise ValueError(f"value search supports hidden <= 128 (got {self.hidden})")
         dev = net.fc1.weight.device
         ps = [t.detach().float().contiguous() for t in (net.fc1.weight, net.fc1.bias, net.value_head.weight,
                                                          net.value_head.bias)]

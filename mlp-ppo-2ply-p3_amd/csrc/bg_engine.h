@@ -417,4 +417,6 @@ struct bgx_engine {
     hipStream_t search_side;  // 2-ply: second stream for the concurrent enumerator (created on demand)
     hipEvent_t search_ev[5];  // 2-ply phase marks: start, enumerated, evaluated, fork, join
     float search_ms[2];       // last bgx_two_ply call, round 0: enumeration ms, evaluation ms
+    void* oneply_ws;          // bgx_one_ply workspace (rows sized for B x max_moves)
+    size_t oneply_ws_bytes;
 };

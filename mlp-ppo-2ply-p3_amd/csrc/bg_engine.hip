@@ -505,7 +505,7 @@ int bgx_engine_destroy(bgx_engine* e) {
     (void)hipSetDevice(e->device);
     Args& A = e->a;
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, e->ovf_base, A.ovf_queue, A.err,
-                    e->slow_tables, e->search_ws, e->search_pool, A.stamps, e->perm, A.cls, e->order_cnt};
+                    e->slow_tables, e->search_ws, e->search_pool, e->oneply_ws, A.stamps, e->perm, A.cls, e->order_cnt};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     for (hipEvent_t ev : e->search_ev) if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : e->step_ev) if (ev) (void)hipEventDestroy(ev);

@@ -1,9 +1,16 @@
 // bg_search.hip — 1-ply greedy and 2-ply expectimax over the 21 dice rolls
 //  with the MLP value head (policy_network.py:54-56,72-75) on MFMA.
 //
-// 2-ply, per root lane (board, mover, roll) with legal afterstates a_0..a_{n-1}:
-//   Q(a) = sum_r p_r * min_{b in replies(a, r)} V(enc(b, opponent))       (leaf = a if no reply)
+// 2-ply, per root lane (board, mover m, roll) with legal afterstates a_0..a_{n-1}:
+//   Q(a) = sum_r p_r * min_{b in replies(a, r)} V(enc(b, m))       (leaf = a if no reply)
 //   best = first argmax_a Q(a)
+// Leaves are encoded with the ROOT mover's one-hot, as the reference's
+// expectiminimax evaluates every node for the root player (expect_minmax.py:57-58,
+// 100-143) and as the critic is trained (observation one-hot = player to move,
+// backgammon_env.py:193-196: after the reply, m is to move); the opponent picks
+// the reply that minimises m's value.
+// 1-ply: V(enc(a, m)) for every afterstate (legal_board_features' one-hot), first
+// argmax -- the same evaluator on the "no reply" leaf of each row.
 // Work item ("job") = (afterstate row, roll r).  The pipeline is decoupled:
 //   k_rows    one wave per row: the afterstate a as a 64-byte record + the
 //             mover's side of a (16 B) for the evaluator;
@@ -19,6 +26,7 @@
 //             f16 values, W1 split hi+lo on v_mfma_f32_32x32x16_f16, value head
 //             in registers, segmented min per job + atomicMin into minv[job];
 //   k_two_ply_reduce  Q(a) and the first argmax.
+// 1-ply: k_scan, k_expand, k_rows (row keys), k_eval_rows (V per row), k_one_ply_reduce.
 // The reference's filter_full_moves_by_max_submoves (get_all_moves.py:73-94) is
 // applied by the evaluator: a leaf counts iff its sub-move count equals the
 // job's final maximum (written at job end), which is exactly "first insertion
@@ -39,18 +47,13 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-constexpr int kK1 = 99;            // 198 / 2 k-steps of 32x32x2 (f32 section, 1-ply)
-constexpr int kKB = 13;            // 208 / 16 k-steps of 32x32x16 (f16 section, 2-ply)
+constexpr int kKB = 13;            // 208 / 16 k-steps of v_mfma_f32_32x32x16_f16
 constexpr int kSlowQueue = 1 << 20;
 constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
 constexpr uint32_t kTagNone = 0xFFFFFFFFu;
 constexpr int kLogLight = 8;       // non-doubles reply enumeration: 256-slot table (4 KiB)
 constexpr int kMaxRounds = 256;
 
-__constant__ float kOff15s[16] = {
-    0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
-    6.0f / 15.0f, 7.0f / 15.0f, 8.0f / 15.0f, 9.0f / 15.0f, 10.0f / 15.0f, 11.0f / 15.0f,
-    12.0f / 15.0f, 13.0f / 15.0f, 14.0f / 15.0f, 15.0f / 15.0f};
 // get_all_dice_rolls_tensor (get_all_dice_rolls.py:5-34): (1,1),(1,2),...,(6,6)
 __constant__ uint8_t kRoll0[21] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6};
 __constant__ uint8_t kRoll1[21] = {1, 2, 3, 4, 5, 6, 2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6, 6};
@@ -58,12 +61,8 @@ __constant__ uint8_t kRoll1[21] = {1, 2, 3, 4, 5, 6, 2, 3, 4, 5, 6, 3, 4, 5, 6, 
 __constant__ uint8_t kNdRoll[15] = {1, 2, 3, 4, 5, 7, 8, 9, 10, 12, 13, 14, 16, 17, 19};
 __constant__ uint8_t kDbRoll[6] = {0, 6, 11, 15, 18, 20};
 
-__device__ __forceinline__ int hid(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-
-// Value net packed for MFMA (bgx_value_pack), in floats:
-//   f32 section (1-ply):  w1p [99][T][64], b1p [T][16][64], wvp [T][16][64]
-//                         (= value_head.weight[32t + hid(r, l>>5)]), bv, 3 pad
-//   f16 section (2-ply):  hdr [4] (e1 as int bits), then NT = ceil(H/16) tiles of
+// Value net packed for MFMA (bgx_value_pack), in floats (H <= 128):
+//                         hdr [4] (e1 as int bits), then NT = ceil(H/16) tiles of
 //                         16 hidden units with their hi AND lo parts in one 32-row
 //                         MFMA tile (row m: unit 16t + (m&7) + 8(m>>4), part (m>>3)&1):
 //     w1q [13][NT][64] x uint4   lane l: the 8 f16 of row l&31 at k = kperm(kb, l>>5, i),
@@ -74,9 +73,6 @@ __device__ __forceinline__ int hid(int r, int h) { return (r & 3) + 8 * (r >> 2)
 // The features are then exact small integers / halves in f16, so one hi and one
 // lo MFMA product give fp32-grade accuracy, and hi + lo of a unit are summed
 // from two accumulator registers of the same lane.
-struct VNet { const float* w1p; const float* b1p; const float* wvp; float bv; };
-
-__host__ __device__ inline int sz_f32(int T) { return kK1 * T * 64 + 2 * T * 16 * 64 + 4; }
 __host__ __device__ inline int sz_f16(int NT) { return 4 + kKB * NT * 64 * 4 + NT * 8 * 64; }
 
 constexpr int kFeatBias = -2;
@@ -94,60 +90,6 @@ __host__ __device__ inline int kperm(int kb, int h, int i) {
     if (h) return -1;
     const int ex[8] = {96, 97, 194, 195, 196, 197, kFeatBias, -1};
     return ex[i];
-}
-
-// Feature k of the board (root bytes `ab` in LDS) after player q moved to the
-// afterstate with key (klo, khi, k3): q's counts come from the key nibbles, the
-// other side's from ab minus the hit blots; one-hot = `cur`.
-__device__ __forceinline__ float feat_key(const uint8_t* ab, uint64_t klo, uint32_t khi, uint32_t k3, int q, int cur,
-                                          int k) {
-    if (k >= 196) return (k == 196) == (cur == 0) ? 1.0f : 0.0f;
-    const int P = k >= 98 ? 1 : 0;
-    const int g = k - 98 * P;
-    const uint32_t hits = k3 >> 8;
-    if (g < 96) {
-        const int pt = g >> 2, u = g & 3;
-        int n;
-        if (P == q) {
-            const uint64_t w = pt < 16 ? klo : (uint64_t)khi;
-            n = (int)((w >> (4 * (pt & 15))) & 15u);
-        } else {
-            n = (int)ab[P * 24 + pt] - (int)((hits >> pt) & 1u);
-        }
-        if (u < 3) return n > u ? 1.0f : 0.0f;
-        return n >= 3 ? (float)(n - 3) * 0.5f : 0.0f;
-    }
-    if (g == 96) {
-        const int bar = P == q ? (int)(k3 & 15u) : (int)ab[48 + P] + __builtin_popcount(hits);
-        return (float)bar * 0.5f;
-    }
-    const int off = P == q ? (int)((k3 >> 4) & 15u) : (int)ab[50 + P];
-    return kOff15s[off & 15];
-}
-
-// V for the 32 rows held by lanes (row j = lane & 31; both lane halves return it).
-template <int T>
-__device__ __forceinline__ float eval_rows(const VNet& vn, const uint8_t* ab, uint64_t klo, uint32_t khi, uint32_t k3,
-                                           int q, int cur) {
-    const int l = threadIdx.x & 63, h = l >> 5;
-    f32x16 x1[T];
-    #pragma unroll
-    for (int t = 0; t < T; ++t)
-        #pragma unroll
-        for (int r = 0; r < 16; ++r) x1[t][r] = vn.b1p[(t * 16 + r) * 64 + l];
-    for (int kk = 0; kk < kK1; ++kk) {
-        const float b = feat_key(ab, klo, khi, k3, q, cur, 2 * kk + h);
-        #pragma unroll
-        for (int t = 0; t < T; ++t)
-            x1[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(vn.w1p[(kk * T + t) * 64 + l], b, x1[t], 0, 0, 0);
-    }
-    float v = 0.0f;
-    #pragma unroll
-    for (int t = 0; t < T; ++t)
-        #pragma unroll
-        for (int r = 0; r < 16; ++r) v = fmaf(fmaxf(x1[t][r], 0.0f), vn.wvp[(t * 16 + r) * 64 + l], v);
-    v += __shfl_xor(v, 32);
-    return v + vn.bv;
 }
 
 __device__ __forceinline__ float wave_min(float v) {
@@ -409,11 +351,14 @@ __global__ __launch_bounds__(64) void k_enum_slow(S2 S, uint4* tables) {
 }
 
 // The afterstate of every row (root lane, legal move a): 64-byte record for the
-// enumerators and the mover's side of a (nibbles, bar, off, replier q) for k_eval.
-__global__ __launch_bounds__(256) void k_rows(Args A, const int32_t* row_lane, const int32_t* lane_off, int32_t rows,
-                                              uint8_t* rowrec, uint4* rowside) {
+// enumerators and the mover's side of a (nibbles, bar, off, replier q) for k_eval;
+// rowkey (1-ply, may be null): the replier's side of a as a leaf key (no hits) --
+// the row's "no reply" leaf.  The row count comes from *nrows (k_scan's total).
+__global__ __launch_bounds__(256) void k_rows(Args A, const int32_t* row_lane, const int32_t* lane_off,
+                                              const int64_t* nrows, uint8_t* rowrec, uint4* rowside, uint4* rowkey) {
     const int l = lane_id();
     const int nw = gridDim.x * (blockDim.x >> 6);
+    const int rows = (int)*nrows;
     for (int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < rows; row += nw) {
         const int lane_g = row_lane[row];
         const int a = row - lane_off[lane_g];
@@ -425,7 +370,12 @@ __global__ __launch_bounds__(256) void k_rows(Args A, const int32_t* row_lane, c
         s = apply_move(s, m, mover);
         const int bva = bytes_from_node(bv, s, mover);
         const int q = 1 - mover;
-        rowrec[(size_t)row * 64 + l] = (uint8_t)(l < 52 ? bva : (l == 52 ? q : 0));
+        if (rowrec) rowrec[(size_t)row * 64 + l] = (uint8_t)(l < 52 ? bva : (l == 52 ? q : 0));
+        if (rowkey) {
+            uint32_t bq;
+            const Node sq = node_from_bytes(bva, q, bq);
+            if (l == 0) rowkey[row] = make_uint4((uint32_t)sq.lo, (uint32_t)(sq.lo >> 32), sq.hi, sq.k3 & 0xFFu);
+        }
         if (l == 0)
             rowside[row] = make_uint4((uint32_t)s.lo, (uint32_t)(s.lo >> 32), s.hi,
                                       (s.k3 & 15u) | (((s.k3 >> 4) & 15u) << 4) | ((uint32_t)q << 8));
@@ -478,6 +428,7 @@ __device__ __forceinline__ LeafRow load_row(const EvalArgs& E, const LeafRaw& r)
 
 // Both sides of the reply afterstate: the replier q's from the key, the root
 // mover's = its side of a minus the blots q hit (a hit point held exactly one).
+// The one-hot is the root mover's, 1 - q (feat16).
 __device__ __forceinline__ Leaf make_leaf(const LeafRaw& r, const LeafRow& w) {
     const uint4 key = r.key, rs = w.rs;
     Leaf L;
@@ -552,7 +503,7 @@ __device__ __forceinline__ f16x8 feat16(const Leaf& L, int kb, int h) {
     } else if (h == 0) {
         v = make_uint4(f16_pair(L.bar[0] | (L.off[0] << 16), 0.5f, 1.0f),
                        f16_pair(L.bar[1] | (L.off[1] << 16), 0.5f, 1.0f),
-                       L.q == 0 ? 0x3C00u : 0x3C000000u, 0x3C00u);
+                       L.q == 1 ? 0x3C00u : 0x3C000000u, 0x3C00u);     // one-hot of the root mover 1 - q
     } else {
         v = make_uint4(0u, 0u, 0u, 0u);
     }
@@ -565,28 +516,84 @@ __device__ __forceinline__ int ord_f32(float v) {
 }
 __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
 
-// Pool tiles of 64 leaves (two 32-column MFMA tiles sharing the weight
-// fragments): X1s = [W1 | b1]s . [F | 1]^T on v_mfma_f32_32x32x16_f16, one MFMA per
-// (k-block, 16 hidden units, 32 leaves) -- the units' hi and lo weight parts sit in
-// rows m and m+8 of the same tile (accumulator registers r and r+4 of a lane) --
-// then V = sum wv 2^-e1 relu(hi + lo) + bv, and per job the min over its leaves
-// (leaves of a job are contiguous in the pool): segmented min over each 32-column
-// tile, one atomicMin per job segment.  Workgroup = 4 waves sharing the packed
-// weights in LDS (NT = 3 for H = 40: 39 KiB); every wave walks its own tiles with
-// the next tile's pool entries in flight during the current tile's MFMAs.
-constexpr int kEvalWaves = 4;
+// V of 2 x 32 leaves (column c = lane & 31 of tile n; both lane halves return it):
+// X1s = [W1 | b1]s . [F | 1]^T on v_mfma_f32_32x32x16_f16, one MFMA per (k-block,
+// 16 hidden units, 32 leaves) -- the units' hi and lo weight parts sit in rows m
+// and m+8 of the same tile (accumulator registers r and r+4 of a lane) -- then
+// V = sum wv 2^-e1 relu(hi + lo) + bv.  The weight fragments come from LDS (wq,
+// wvs) and are shared by the two leaf tiles.  At most 4 unit tiles (64 units) are
+// accumulated per pass (2 x 4 x 16 accumulator VGPRs); H = 128 takes two passes
+// over K, regenerating the features.  `z` = an opaque zero offset that keeps the
+// LDS fragment reads inside the loops.
 template <int NT>
-__global__ __launch_bounds__(64 * kEvalWaves) void k_eval(EvalArgs E) {
+__device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z, float bias,
+                                            float (&v)[2]) {
+    constexpr int G = NT < 4 ? NT : 4;
+    const int l = lane_id(), h = l >> 5;
+    v[0] = 0.0f;
+    v[1] = 0.0f;
+    // passes kept apart (not unrolled): interleaved, two passes' accumulators spill
+    #pragma unroll 1
+    for (int g0 = 0; g0 < NT; g0 += G) {
+        f32x16 x[2][G];
+        #pragma unroll
+        for (int kb = 0; kb < kKB; ++kb) {
+            const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
+            #pragma unroll
+            for (int t = 0; t < G; ++t) {
+                if (g0 + t < NT) {
+                    const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + g0 + t) * 64 + l + z]);
+                    const f32x16 c0 = kb == 0 ? (f32x16){} : x[0][t];
+                    const f32x16 c1 = kb == 0 ? (f32x16){} : x[1][t];
+                    x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, c0, 0, 0, 0);
+                    x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, c1, 0, 0, 0);
+                }
+            }
+        }
+        #pragma unroll
+        for (int n = 0; n < 2; ++n)
+            #pragma unroll
+            for (int t = 0; t < G; ++t)
+                if (g0 + t < NT)
+                    #pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const int r = j < 4 ? j : j + 4;
+                        v[n] = fmaf(fmaxf(x[n][t][r] + x[n][t][r + 4], 0.0f), wvs[((g0 + t) * 8 + j) * 64 + l + z],
+                                    v[n]);
+                    }
+    }
+    #pragma unroll
+    for (int n = 0; n < 2; ++n) v[n] += __shfl_xor(v[n], 32) + bias;
+}
+
+// workgroup shape of the evaluators: 4 waves (NT <= 4: <= 52 KiB of weights in LDS,
+// several workgroups per CU) or 8 waves (H = 128: 120 KiB, one workgroup per CU,
+// two waves per SIMD)
+template <int NT> struct EvalShape { static constexpr int kWaves = NT <= 4 ? 4 : 8; };
+
+template <int NT>
+__device__ __forceinline__ void stage_weights(uint4* wq, float* wvs, const uint4* w1q, const float* wvq) {
+    for (int i = threadIdx.x; i < kKB * NT * 64; i += blockDim.x) wq[i] = w1q[i];
+    for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = wvq[i];
+    __syncthreads();
+}
+
+// 2-ply: pool tiles of 64 leaves; per job the min over its leaves (leaves of a job
+// are contiguous in the pool): segmented min over each 32-column tile, one
+// atomicMin per job segment.  Workgroups share the packed weights in LDS; every
+// wave walks its own tiles with the next tile's pool entries in flight during the
+// current tile's MFMAs.
+template <int NT>
+__global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) void k_eval(EvalArgs E) {
+    constexpr int W = EvalShape<NT>::kWaves;
     __shared__ uint4 wq[kKB * NT * 64];
     __shared__ float wvs[NT * 8 * 64];
     const int l = lane_id(), h = l >> 5, c = l & 31;
-    for (int i = threadIdx.x; i < kKB * NT * 64; i += blockDim.x) wq[i] = E.w1q[i];
-    for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = E.wvq[i];
-    __syncthreads();
+    stage_weights<NT>(wq, wvs, E.w1q, E.wvq);
     const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
     const unsigned long long tiles = used / 64;
-    const unsigned long long stride = (unsigned long long)gridDim.x * kEvalWaves;
-    unsigned long long tile = *E.lo / 64 + (unsigned long long)blockIdx.x * kEvalWaves + (threadIdx.x >> 6);
+    const unsigned long long stride = (unsigned long long)gridDim.x * W;
+    unsigned long long tile = *E.lo / 64 + (unsigned long long)blockIdx.x * W + (threadIdx.x >> 6);
     if (tile >= tiles) return;
     LeafRaw raw[2];
     LeafRow row[2];
@@ -596,53 +603,93 @@ __global__ __launch_bounds__(64 * kEvalWaves) void k_eval(EvalArgs E) {
         Leaf L[2];
         #pragma unroll
         for (int n = 0; n < 2; ++n) L[n] = make_leaf(raw[n], row[n]);
-        // an opaque zero offset per tile keeps the LDS fragment reads inside the loop
-        // (hoisted, the 39 fragments would take 156 registers)
         int z = 0;
         __asm__ volatile("" : "+s"(z));
         const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
         #pragma unroll
         for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
-        f32x16 x[2][NT];
-        #pragma unroll
-        for (int kb = 0; kb < kKB; ++kb) {
-            const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
-            #pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + t) * 64 + l + z]);
-                const f32x16 c0 = kb == 0 ? (f32x16){} : x[0][t];
-                const f32x16 c1 = kb == 0 ? (f32x16){} : x[1][t];
-                x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, c0, 0, 0, 0);
-                x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, c1, 0, 0, 0);
-            }
-        }
+        float v[2];
+        eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
         #pragma unroll
         for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
         #pragma unroll
         for (int n = 0; n < 2; ++n) {
-            float v = 0.0f;
-            #pragma unroll
-            for (int t = 0; t < NT; ++t)
-                #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int r = j < 4 ? j : j + 4;
-                    v = fmaf(fmaxf(x[n][t][r] + x[n][t][r + 4], 0.0f), wvs[(t * 8 + j) * 64 + l + z], v);
-                }
-            v += __shfl_xor(v, 32);
-            v += E.bv;
             const int jb = L[n].job;
-            v = L[n].valid ? v : INFINITY;
+            float vv = L[n].valid ? v[n] : INFINITY;
             // segmented min over equal-job runs of the 32 columns (lanes 0..31 == 32..63)
             #pragma unroll
             for (int o = 1; o < 32; o <<= 1) {
-                const float v2 = __shfl_down(v, o, 32);
+                const float v2 = __shfl_down(vv, o, 32);
                 const int j2 = __shfl_down(jb, o, 32);
-                if (c + o < 32 && j2 == jb) v = fminf(v, v2);
+                if (c + o < 32 && j2 == jb) vv = fminf(vv, v2);
             }
             const int jp = __shfl_up(jb, 1, 32);
-            if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(v));
+            if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
         }
     }
+}
+
+// 1-ply: V of every row's afterstate (the row's "no reply" leaf: rowkey + rowside),
+// 64 rows per tile, grid-stride over ceil(*nrows / 64) tiles.
+struct EvalRowsArgs {
+    const uint4* rowkey;
+    const uint4* rowside;
+    const int64_t* nrows;
+    float* vrow;
+    const uint4* w1q;
+    const float* wvq;
+    float bv;
+};
+
+template <int NT>
+__global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) void k_eval_rows(EvalRowsArgs E) {
+    constexpr int W = EvalShape<NT>::kWaves;
+    __shared__ uint4 wq[kKB * NT * 64];
+    __shared__ float wvs[NT * 8 * 64];
+    const int l = lane_id(), h = l >> 5, c = l & 31;
+    stage_weights<NT>(wq, wvs, E.w1q, E.wvq);
+    const long long rows = *E.nrows;
+    const long long tiles = (rows + 63) / 64;
+    for (long long tile = (long long)blockIdx.x * W + (threadIdx.x >> 6); tile < tiles;
+         tile += (long long)gridDim.x * W) {
+        Leaf L[2];
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            const long long r = tile * 64 + 32 * n + c;
+            const bool in = r < rows;
+            const LeafRaw raw{in ? E.rowkey[r] : make_uint4(0u, 0u, 0u, 0u), in ? 0u : kTagNone};
+            const LeafRow rw{in ? E.rowside[r] : make_uint4(0u, 0u, 0u, 0u), 0u};
+            L[n] = make_leaf(raw, rw);
+        }
+        int z = 0;
+        __asm__ volatile("" : "+s"(z));
+        float v[2];
+        eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) {
+            const long long r = tile * 64 + 32 * n + c;
+            if (h == 0 && r < rows) E.vrow[r] = v[n];
+        }
+    }
+}
+
+// 1-ply choice per lane: first argmax of V over its rows (values_out row a = V(a)).
+__global__ void k_one_ply_reduce(Args A, const int32_t* lane_off, const float* vrow, int32_t* best, float* bestv,
+                                 float* vout) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.B) return;
+    const uint8_t* rr = A.lanes + (size_t)i * 64;
+    const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
+    const float* v = vrow + lane_off[i];
+    float bv = -INFINITY;
+    int ba = 0;
+    for (int a = 0; a < n; ++a) {
+        const float x = v[a];
+        if (vout) vout[(size_t)i * A.max_moves + a] = x;
+        if (x > bv) { bv = x; ba = a; }
+    }
+    best[i] = ba;
+    if (bestv) bestv[i] = n ? bv : 0.0f;
 }
 
 // Q(a) = sum_r p_r minv[a][r] (fp32, r in roll order), first argmax.
@@ -754,66 +801,13 @@ __global__ void k_expand(Args A, const int32_t* lane_off, int32_t* row_lane) {
     for (int a = 0; a < n; ++a) row_lane[lane_off[i] + a] = i;
 }
 
-// 1-ply: every lane's afterstates a (mover's one-hot), first argmax V(a).
-template <int T>
-__global__ __launch_bounds__(64) void k_one_ply(Args A, VNet vn, int32_t* best, float* bestv, float* vout) {
-    __shared__ uint8_t ab[64];
-    const int gi = blockIdx.x;
-    const int l = threadIdx.x & 63, j = l & 31;
-    const int bv = load_rec(A, gi);
-    const int mover = rd(bv, R_CUR);
-    const int n = rd(bv, R_NM0) | (rd(bv, R_NM1) << 8);
-    ab[l] = (uint8_t)bv;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    uint32_t blocked;
-    const Node s0 = node_from_bytes(bv, mover, blocked);
-    float bvv = -INFINITY;
-    int ba = 0;
-    for (int base = 0; base < n; base += 32) {
-        const int a = base + (j < n - base ? j : 0);
-        const Node s = apply_move(s0, A.moves[(size_t)gi * A.max_moves + a], mover);   // per-lane move
-        const float v = eval_rows<T>(vn, ab, s.lo, s.hi, s.k3, mover, mover);
-        if (vout && l < 32 && base + j < n) vout[(size_t)gi * A.max_moves + base + j] = v;
-        float key = j < n - base ? v : -INFINITY;
-        int idx = base + j;
-        #pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) {     // first argmax over the 32 rows (lanes 0..31 == 32..63)
-            const float k2 = __shfl_xor(key, o);
-            const int i2 = __shfl_xor(idx, o);
-            if (k2 > key || (k2 == key && i2 < idx)) { key = k2; idx = i2; }
-        }
-        if (key > bvv) { bvv = key; ba = idx; }
-    }
-    if (l == 0) { best[gi] = ba; if (bestv) bestv[gi] = n ? bvv : 0.0f; }
-}
-
-__global__ void k_value_pack(const float* W1, const float* b1, const float* wv, const float* bv, int H, int T,
-                             float* w1p, float* b1p, float* wvp, float* bvp) {
-    const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int n1 = kK1 * T * 64, nb = T * 16 * 64;
-    if (tid < n1) {
-        const int l = tid % 64, t = (tid / 64) % T, kk = tid / (64 * T);
-        const int hrow = 32 * t + (l & 31);
-        w1p[tid] = hrow < H ? W1[(size_t)hrow * 198 + 2 * kk + (l >> 5)] : 0.0f;
-    } else if (tid < n1 + 2 * nb) {
-        const int i = (tid - n1) % nb;
-        const bool isb = tid < n1 + nb;
-        const int l = i % 64, r = (i / 64) % 16, t = i / (64 * 16);
-        const int hrow = 32 * t + hid(r, l >> 5);
-        if (isb) b1p[i] = hrow < H ? b1[hrow] : 0.0f;
-        else wvp[i] = hrow < H ? wv[hrow] : 0.0f;
-    } else if (tid == n1 + 2 * nb) {
-        bvp[0] = bv[0];
-    }
-}
-
 }  // namespace
 
 extern int bgx_internal_fail(hipError_t e);
 #define SCK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return bgx_internal_fail(_e); } while (0)
 
-static int value_tiles(int H) { return H <= 32 ? 1 : 2; }   // f32 section (1-ply): 32-unit tiles
-static int value_tiles16(int H) { return (H + 15) / 16; }   // f16 section (2-ply): 16 units per tile
+static int value_tiles16(int H) { return (H + 15) / 16; }   // 16 hidden units (hi + lo rows) per MFMA tile
+constexpr int kMaxHidden = 128;                              // 8 tiles: 120 KiB of weights in LDS
 
 template <typename K>
 static int persistent_grid(const bgx_engine* e, K kernel, int per_cu_cap) {
@@ -825,59 +819,96 @@ static int persistent_grid(const bgx_engine* e, K kernel, int per_cu_cap) {
     return cus * occ;
 }
 
+typedef void (*EvalFn)(EvalArgs);
+typedef void (*EvalRowsFn)(EvalRowsArgs);
+static EvalFn eval_kernel(int NT) {
+    switch (NT) {
+        case 1: return k_eval<1>; case 2: return k_eval<2>; case 3: return k_eval<3>; case 4: return k_eval<4>;
+        case 5: return k_eval<5>; case 6: return k_eval<6>; case 7: return k_eval<7>; default: return k_eval<8>;
+    }
+}
+static EvalRowsFn eval_rows_kernel(int NT) {
+    switch (NT) {
+        case 1: return k_eval_rows<1>; case 2: return k_eval_rows<2>; case 3: return k_eval_rows<3>;
+        case 4: return k_eval_rows<4>; case 5: return k_eval_rows<5>; case 6: return k_eval_rows<6>;
+        case 7: return k_eval_rows<7>; default: return k_eval_rows<8>;
+    }
+}
+static int eval_waves(int NT) { return NT <= 4 ? 4 : 8; }
+
+// resident workgroups of an evaluator over the whole device
+template <typename K>
+static int eval_grid(const bgx_engine* e, K kernel, int NT) {
+    int occ = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, 64 * eval_waves(NT), 0) != hipSuccess || occ <= 0)
+        occ = 1;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || ncu <= 0)
+        ncu = 256;
+    return occ * ncu;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 extern "C" {
 
 int bgx_value_packed_size(int32_t hidden) {
-    if (hidden <= 0 || hidden > 64) return BGX_EINVAL;
-    return sz_f32(value_tiles(hidden)) + sz_f16(value_tiles16(hidden));
+    if (hidden <= 0 || hidden > kMaxHidden) return BGX_EINVAL;
+    return sz_f16(value_tiles16(hidden));
 }
 
 int bgx_value_pack(const float* W1, const float* b1, const float* wv, const float* bv, int32_t hidden, float* packed,
                    void* stream) {
     const int total = bgx_value_packed_size(hidden);
     if (total < 0 || !W1 || !b1 || !wv || !bv || !packed) return BGX_EINVAL;
-    const int T = value_tiles(hidden);
-    float* w1p = packed;
-    float* b1p = w1p + kK1 * T * 64;
-    float* wvp = b1p + T * 16 * 64;
-    float* bvp = wvp + T * 16 * 64;
-    const int n32 = sz_f32(T);
-    hipLaunchKernelGGL(k_value_pack, dim3((n32 + 255) / 256), dim3(256), 0, (hipStream_t)stream, W1, b1, wv, bv, hidden,
-                       T, w1p, b1p, wvp, bvp);
-    SCK(hipGetLastError());
-    float* f16s = packed + n32;
     const int NT = value_tiles16(hidden);
     hipLaunchKernelGGL(k_value_pack16, dim3(1), dim3(1024), 0, (hipStream_t)stream, W1, b1, wv, hidden, NT,
-                       (int*)f16s, (_Float16*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4);
+                       (int*)packed, (_Float16*)(packed + 4), packed + 4 + kKB * NT * 64 * 4);
     SCK(hipGetLastError());
     return BGX_OK;
-}
-
-static VNet make_vnet(const float* packed, int hidden, float bv_host) {
-    const int T = value_tiles(hidden);
-    VNet v;
-    v.w1p = packed;
-    v.b1p = v.w1p + kK1 * T * 64;
-    v.wvp = v.b1p + T * 16 * 64;
-    v.bv = bv_host;
-    return v;
 }
 
 int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value_bias, int32_t* best_out,
                 float* bestv_out, float* values_out, void* stream) {
     if (!e || !vpacked || !best_out || bgx_value_packed_size(hidden) < 0) return BGX_EINVAL;
     SCK(hipSetDevice(e->device));
-    const VNet vn = make_vnet(vpacked, hidden, value_bias);
     hipStream_t s = (hipStream_t)stream;
-    if (value_tiles(hidden) == 1)
-        hipLaunchKernelGGL(k_one_ply<1>, dim3(e->a.B), dim3(64), 0, s, e->a, vn, best_out, bestv_out, values_out);
-    else
-        hipLaunchKernelGGL(k_one_ply<2>, dim3(e->a.B), dim3(64), 0, s, e->a, vn, best_out, bestv_out, values_out);
+    Args& A = e->a;
+    const size_t B = (size_t)A.B, R = B * (size_t)A.max_moves;
+    // [lane_off B i32][row total i64][row_lane R i32][rowside R][rowkey R][vrow R f32]: sized for
+    // the worst case, so the pass runs without a host sync (the row count stays on the device)
+    const size_t o_tot = align256(B * 4), o_rl = o_tot + 256, o_side = align256(o_rl + R * 4),
+                 o_key = align256(o_side + R * 16), o_v = align256(o_key + R * 16), need = align256(o_v + R * 4);
+    if (e->oneply_ws_bytes < need) {
+        SCK(hipStreamSynchronize(s));
+        if (e->oneply_ws) SCK(hipFree(e->oneply_ws));
+        e->oneply_ws = nullptr;
+        e->oneply_ws_bytes = 0;
+        SCK(hipMalloc(&e->oneply_ws, need));
+        e->oneply_ws_bytes = need;
+    }
+    char* ws = (char*)e->oneply_ws;
+    int32_t* lane_off = (int32_t*)ws;
+    int64_t* total = (int64_t*)(ws + o_tot);
+    int32_t* row_lane = (int32_t*)(ws + o_rl);
+    uint4* rowside = (uint4*)(ws + o_side);
+    uint4* rowkey = (uint4*)(ws + o_key);
+    float* vrow = (float*)(ws + o_v);
+    const int NT = value_tiles16(hidden);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, lane_off, total);
+    hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
+    // ~20 legal moves per lane on average: one wave per ~5 rows at B = 4,096
+    const size_t gr = B * 6 < 16384 ? (B * 6 > 64 ? B * 6 : 64) : 16384;
+    hipLaunchKernelGGL(k_rows, dim3((unsigned)gr), dim3(256), 0, s, A, row_lane, lane_off, total, nullptr, rowside,
+                       rowkey);
+    const EvalRowsFn kr = eval_rows_kernel(NT);
+    const EvalRowsArgs E{rowkey, rowside, total, vrow, (const uint4*)(vpacked + 4), vpacked + 4 + kKB * NT * 64 * 4,
+                         value_bias};
+    hipLaunchKernelGGL(kr, dim3(eval_grid(e, kr, NT)), dim3(64 * eval_waves(NT)), 0, s, E);
+    hipLaunchKernelGGL(k_one_ply_reduce, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, vrow, best_out,
+                       bestv_out, values_out);
     SCK(hipGetLastError());
     return BGX_OK;
 }
-
-static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value_bias, int32_t* best_out,
                 float* bestq_out, float* q_out, uint64_t* stats_host, void* stream) {
@@ -948,7 +979,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         SCK(hipMemsetAsync(minv, 0x7F, (size_t)jobs * 4, s));
         SCK(hipMemsetAsync(maxlen, 0xFF, (size_t)jobs, s));
         hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
-                           lane_off, rows, rowrec, rowside);
+                           lane_off, &ctr->rows, rowrec, rowside, nullptr);
         SCK(hipGetLastError());
         S2 S{rowrec, 0, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
@@ -980,8 +1011,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         }
         const bool dbg = getenv("BGX_2PLY_DEBUG") != nullptr;
         const int NT = value_tiles16(hidden);
-        const float* f16s = vpacked + sz_f32(value_tiles(hidden));
-        const VNet vn = make_vnet(vpacked, hidden, value_bias);
+        const float* f16s = vpacked;
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4, value_bias};
         int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
@@ -1012,11 +1042,8 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         E.keys = S.keys;
         E.tags = S.tags;
         S.cap = E.cap = (unsigned long long)pcap;
-        int g_eval = 0, ncu = 0;
-        SCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->device));
-        void (*keval)(EvalArgs) = NT == 1 ? k_eval<1> : NT == 2 ? k_eval<2> : NT == 3 ? k_eval<3> : k_eval<4>;
-        SCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&g_eval, keval, 64 * kEvalWaves, 0));
-        g_eval = (g_eval > 0 ? g_eval : 1) * (ncu > 0 ? ncu : 256);
+        const EvalFn keval = eval_kernel(NT);
+        const int g_eval = eval_grid(e, keval, NT);
         if (!e->search_ev[0])
             for (hipEvent_t& ev : e->search_ev) SCK(hipEventCreate(&ev));
         const char* ov = getenv("BGX_2PLY_OVERLAP");    // "0": enumerators back to back (A/B)
@@ -1032,7 +1059,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         }
         SCK(hipEventRecord(e->search_ev[0], s));
         auto eval = [&](hipStream_t st) {
-            hipLaunchKernelGGL(keval, dim3(g_eval), dim3(64 * kEvalWaves), 0, st, E);
+            hipLaunchKernelGGL(keval, dim3(g_eval), dim3(64 * eval_waves(NT)), 0, st, E);
         };
         // retry rounds run few waves: every wave holding a block wastes its unused
         // part, and a round must leave pool for its jobs to finish (progress with any pool)

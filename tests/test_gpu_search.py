@@ -1,5 +1,8 @@
 """1-ply / 2-ply search kernels vs a composition of the oracle (move lists,
-afterstates, features) and the torch fp32 value head.  Tolerance 1e-5 on V and Q."""
+afterstates, features) and the torch fp32 value head, at H = 40 (C2/C4) and at
+the reference's H = 128 (agent/config.py:8; golden G5 weights).  Tolerance 1e-5
+on V and Q.  2-ply leaves carry the root mover's one-hot (the reference's
+evaluate_board(board, current_player), moves/expect_minmax.py:57-58, 100-143)."""
 import numpy as np
 import pytest
 import torch
@@ -12,15 +15,17 @@ ROLLS = [(a, b) for a in range(1, 7) for b in range(a, 7)]
 PROBS = np.array([1 / 36 if a == b else 2 / 36 for a, b in ROLLS], np.float32)
 
 
-@pytest.fixture(scope="module")
-def setup(golden):
+@pytest.fixture(scope="module", params=[40, 128])
+def setup(golden, request):
     import bgx
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead
+    H = request.param
     mlp = golden("mlp")
-    net = PolicyNet(hidden_size=40).cuda()
-    net.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in mlp.items()
-                         if k.startswith("h40_") and not k.endswith(("logits", "values"))})
+    net = PolicyNet(hidden_size=H).cuda()
+    pre = f"h{H}_"
+    net.load_state_dict({k[len(pre):]: torch.from_numpy(v) for k, v in mlp.items()
+                         if k.startswith(pre) and not k.endswith(("logits", "values"))})
     B = 48
     eng = bgx.Engine(batch=B, max_moves=500, dice="mt", auto_reset=True)
     eng.seed(np.arange(500, 500 + B, dtype=np.uint32))
@@ -76,9 +81,9 @@ def test_two_ply_vs_oracle_composition(setup):
                 for r, roll in enumerate(ROLLS):
                     reps, cnt = O.movegen(aft, opp, roll, cap=4096)
                     if cnt == 0:
-                        leaf = [O.features(aft, opp)]
+                        leaf = [O.features(aft, mover)]
                     else:
-                        leaf = [O.features(O.apply_move(aft, opp, int(b)), opp) for b in reps]
+                        leaf = [O.features(O.apply_move(aft, opp, int(b)), mover) for b in reps]
                     acc += float(PROBS[r]) * float(_V(net, leaf).min())
                 Q[a] = acc
             assert np.abs(q[i, :n] - Q).max() < TOL, i

@@ -27,7 +27,7 @@ def Q(board, mover, move, sub_limit=4):
     aft = O.apply_move(board, mover, O.encode_move(subs)); opp = 1 - mover; acc = 0.0
     for r, roll in enumerate(ROLLS):
         reps, cnt = O.movegen(aft, opp, roll, cap=4096)
-        leaf = [O.features(aft, opp)] if cnt == 0 else [O.features(O.apply_move(aft, opp, int(b)), opp) for b in reps]
+        leaf = [O.features(aft, mover)] if cnt == 0 else [O.features(O.apply_move(aft, opp, int(b)), mover) for b in reps]
         acc += float(PROBS[r]) * float(V(leaf).min())
     return acc
 for i in range(4):
