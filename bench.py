@@ -100,29 +100,34 @@ def sum_over_ranks(x: float, ws: int) -> float:
 
 def cpu_baseline(seconds: float):
     """The oracle (C restatement of the reference env, oracle/bgoracle.c) stepping a
-    random legal policy on ONE host core for ~`seconds`: the reported CPU baseline."""
+    random legal policy on the GPU box's host cores: one process per core on the
+    cores this job may use (at most 16, the box's CPU share per GPU), plus a
+    1-core run.  The reference's own Python env cannot run on the box; its timing
+    on the build container (tools/time_reference_env.py, with the port timed
+    beside it as the bridge ratio) is attached from profiles/."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
-    import oracle as O
-    O.build()
-    env = O.Env(seed=0)
-    env.reset()
-    rng = np.random.RandomState(0)
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        for _ in range(200):
-            n = int(env.state()[1][3])
-            _, _, done, _ = env.step(rng.randint(n) if n else 0)
-            if done:
-                env.reset()
-            steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": steps / el, "unit": "env steps/s", "cores": 1, "kind": "port",
-            "sample": f"{steps} random-policy BackgammonEnv.step calls of the C oracle (oracle/bgoracle.c), "
-                      f"1 thread, {el:.1f} s"}
+    import port_bench
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    procs = max(1, min(16, avail))
+    one, one_steps = port_bench.run(seconds, 0)
+    multi, multi_steps = port_bench.run_parallel(seconds, procs)
+    out = {"value": multi, "unit": "env steps/s", "cores": procs, "kind": "port",
+           "sample": f"{multi_steps} random-policy BackgammonEnv.step calls of the C oracle (oracle/bgoracle.c), "
+                     f"{procs} processes x 1 thread, {seconds:.0f} s",
+           "cores_available": avail, "host_cpus": os.cpu_count(),
+           "single_core": {"value": one, "steps": one_steps, "seconds": seconds}}
+    ref = os.path.join(ROOT, "profiles", "cpu_reference_timing.json")
+    if os.path.exists(ref):
+        r = json.load(open(ref))
+        out["reference_python"] = {
+            "value": r["reference_env_steps_per_s"], "unit": "env steps/s", "cores": r["processes"],
+            "where": "build container (the reference never travels to the GPU box)",
+            "port_same_host": r["port_env_steps_per_s"], "port_over_reference": r["port_over_reference"],
+            "estimated_here": multi / r["port_over_reference"], "estimated_here_cores": procs,
+            "estimate_note": "the reference env on this host's cores, estimated as this host's port rate / the "
+                             "port:reference ratio measured on the build container",
+            "source": "profiles/cpu_reference_timing.json (tools/time_reference_env.py)"}
+    return out
 
 
 def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 2):

@@ -225,6 +225,11 @@ int bgx_two_ply_timings(bgx_engine* e, float* ms2);
 /* Last HIP error string of this thread (diagnostics). */
 const char* bgx_last_error(void);
 
+/* Build provenance: sha256 (hex) of the sources and compile flags this library
+ * was built from (bgx._lib.source_hash); smoke() and the tests compare it with
+ * the tree they run from. */
+const char* bgx_build_id(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,6 +6,7 @@ must be present: there is no CPU fallback for the product path.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -52,7 +53,36 @@ SIGNATURES = {
                                        ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, ctypes.c_int64, _P, _P, _I32,
                                        _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
+    "bgx_build_id": (ctypes.c_char_p, []),
 }
+
+_PKG = os.path.dirname(_HERE)
+_CSRC = os.path.join(_PKG, "csrc")
+_HEADER = os.path.join(os.path.dirname(_PKG), "include", "bgx.h")
+BUILD_ID_TAG = b"bgx-build-id:"
+
+
+def source_hash(flags: str = "") -> str:
+    """sha256 over every file under csrc/, include/bgx.h and the compile flags:
+    the build id compiled into libbgx.so (bgx_build_id())."""
+    h = hashlib.sha256()
+    files = sorted(os.path.join(_CSRC, f) for f in os.listdir(_CSRC)
+                   if f.endswith((".hip", ".h", ".cpp"))) + [_HEADER]
+    for f in files:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(flags.encode())
+    return h.hexdigest()
+
+
+def embedded_build_id(path: str = LIB_PATH):
+    """The build id stored in a built library file (read from its bytes, no load)."""
+    if not os.path.exists(path):
+        return None
+    data = open(path, "rb").read()
+    i = data.find(BUILD_ID_TAG)
+    return data[i + len(BUILD_ID_TAG):i + len(BUILD_ID_TAG) + 64].decode() if i >= 0 else None
 
 
 class BgxBuffers(ctypes.Structure):

@@ -754,4 +754,11 @@ int bgx_engine_error(bgx_engine* e, int32_t* err_out) {
 
 const char* bgx_last_error(void) { return g_err.c_str(); }
 
+#ifndef BGX_BUILD_ID
+#define BGX_BUILD_ID "unknown"
+#endif
+// the tag lets build() read the id from the file without loading it
+__attribute__((used)) static const char kBuildId[] = "bgx-build-id:" BGX_BUILD_ID;
+const char* bgx_build_id(void) { return kBuildId + 13; }
+
 }  // extern "C"

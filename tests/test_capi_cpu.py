@@ -41,3 +41,27 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 src = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in src and "bgoracle" not in src, f
+
+
+def test_library_built_from_these_sources():
+    """Build provenance: the id compiled into libbgx.so equals the hash of the
+    current csrc/ + include/ sources and flags (a stale library fails here)."""
+    import __graft_entry__ as G
+    import bgx._lib as L
+    if not os.path.exists(L.LIB_PATH):
+        pytest.skip("libbgx.so not built")
+    want = L.source_hash(" ".join(G.HIPCC_FLAGS))
+    assert L.embedded_build_id() == want
+    assert L.load().bgx_build_id().decode() == want
+
+
+def test_oracle_under_asan():
+    """The CPU oracle built with AddressSanitizer + UBSan (oracle/Makefile `asan`)
+    plays 60 seeded random games (invalid actions, resets, match ends) and
+    enumerates > 500-move positions with a small cap, checking checker
+    conservation; any memory error or UB aborts."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], check=True)
+    r = subprocess.run([os.path.join(ROOT, "oracle", "bgoracle_asan"), "60"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "asan ok" in r.stdout and "runtime error" not in r.stderr
