@@ -358,9 +358,11 @@ def main():
     # record in+out 128, action 4, chosen move 8, new move list 8*n, reward 4, done 1, rng ctr 8+8
     bytes_per_lane = 128 + 4 + 8 + 8 * mean_moves + 4 + 1 + 16
     achieved = Bs * bytes_per_lane / (kern_ms * 1e-3) / 1e9    # one shard's env step per window
-    # HBM bytes per env step (all kernels bgx_step launches: both k_step launches, the
-    # order sort, the overflow tiers) from the committed rocprofv3 PMC passes
-    # (tools/profile.sh -> profiles/latest_summary.json; (2*FETCH_SIZE + WRITE_SIZE)*1024)
+    # HBM bytes per env step of one shard (all kernels bgx_step launches: both k_step
+    # launches, the order sort, the overflow tiers) from the committed rocprofv3 PMC
+    # passes (tools/profile.sh -> profiles/latest_summary.json; (FETCH_SIZE + WRITE_SIZE)
+    # x 1024: the step's 64-B record / 4-8-B scalar reads are single 64-B requests that
+    # FETCH_SIZE counts exactly, calibrated in profiles/r2_fetch_calibration.json)
     traffic, traffic_src, prof_kernels = None, None, None
     prof = os.path.join(ROOT, "profiles", "latest_summary.json")
     if os.path.exists(prof):
@@ -399,7 +401,9 @@ def main():
                                "the light launch on the engine's side stream (event fork-join); HIP events around "
                                "bgx_step on the shard's stream, per shard of games_per_gpu/shards lanes",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/env step",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": f"bytes per env-step launch (one shard of {Bs} lanes)",
+                     "traffic_per_lane_step": traffic / Bs if traffic else None,
+                     "traffic_over_algorithmic": traffic / (Bs * bytes_per_lane) if traffic else None,
                      "traffic_source": traffic_src, "algorithmic_bytes_per_step": Bs * bytes_per_lane, "lanes_per_launch": Bs,
                      "kernel_ms": kern_ms, "bytes_per_lane_step": bytes_per_lane,
                      "rocprof_avg_us": prof_kernels,

@@ -168,7 +168,17 @@ struct Args {
     // into cls; k_order turns the classes into perm (heaviest first) for the next launch.
     int32_t* perm;            // blockIdx -> lane, or null (identity)
     uint8_t* cls;             // [B] predicted cost class, or null
+    int xcd;                  // B % 128 == 0: XCD-aware dispatch (16-lane runs per XCD, bg_engine.hip k_order_*)
 };
+
+// blockIdx -> lane when there is no dispatch order: blocks b, b + 8, ... (one XCD
+// under round-robin placement) take the 16 consecutive lanes of one run, so a
+// run's partial-line loads and stores stay in one XCD's L2.  Identity otherwise.
+__device__ __forceinline__ int lane_of_block(const Args& A, int bi) {
+    if (!A.xcd) return bi;
+    const int r = bi & 127;
+    return (bi & ~127) | ((r & 7) << 4) | (r >> 3);
+}
 
 constexpr int kClasses = 5;
 

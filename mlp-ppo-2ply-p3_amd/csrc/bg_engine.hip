@@ -64,7 +64,7 @@ __global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, flo
     __shared__ uint4 memo_[MEMO == 1 ? kMemoSlots : 1];
     uint4* memo = MEMO == 1 ? memo_ : MEMO == 2 ? tab : nullptr;
     const int bi = (int)blockIdx.x + base;
-    const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : bi;
+    const int gi = A.perm ? (int)ufl((uint32_t)A.perm[bi]) : lane_of_block(A, bi);
     step_lane<PHASE, LOG, MEMO, NO_DOUBLES>(A, gi, tab, memo, actions, obs, reward, done, info);
 }
 
@@ -91,66 +91,87 @@ __global__ __launch_bounds__(64) void k_reset(Args A, const uint8_t* lane_mask, 
 // Next dispatch order = lanes grouped by predicted class (class 0 first), in
 // lane order within a class: a two-pass counting sort over blocks of 1024
 // lanes.  perm is a full permutation of 0..B-1 whatever cls holds.
+//
+// XCD-aware form (B % 128 == 0): the lanes are split into 8 sub-lists by
+// x = (lane >> 4) & 7 (runs of 16 lanes), each sub-list is class-sorted on its
+// own, and position 8k + x holds the k-th lane of sub-list x.  Blocks b and
+// b + 8 of a launch run on one XCD (round-robin placement; the launch bases are
+// multiples of 8), so every 16-lane run -- one 64-B line of the reward / action
+// / n_total arrays, one 128-B line of the Philox counters, 8 lane records -- is
+// stepped by ONE XCD per launch and its partial-line loads and stores meet in
+// that XCD's L2 instead of crossing all eight.  The 8 sub-lists have nearly the
+// same class mix, so the interleave keeps the heaviest-first order.
+constexpr int kXcd = 8, kRun = 16;
 __device__ __forceinline__ int order_class(const uint8_t* cls, int i, int B) {
     return i < B ? min((int)cls[i], kClasses - 1) : kClasses;     // kClasses = padding, never written
 }
 
-// pass 1: cnt[b][c] = lanes of class c in block b
-__global__ __launch_bounds__(1024) void k_order_count(const uint8_t* cls, int32_t* cnt, int B, int32_t* zero_next) {
-    __shared__ int sc[kClasses];
-    const int t = threadIdx.x, i = blockIdx.x * 1024 + t;
+// pass 1: cnt[b][x][c] = lanes of class c in sub-list x of block b (x = 0 when !xcd)
+__global__ __launch_bounds__(1024) void k_order_count(const uint8_t* cls, int32_t* cnt, int B, int32_t* zero_next,
+                                                      int xcd) {
+    __shared__ int sc[kXcd][kClasses];
+    const int t = threadIdx.x, i = blockIdx.x * 1024 + t, w = t >> 6;
     if (blockIdx.x == 0 && t < 4) zero_next[t] = 0;     // the next step's overflow counters
-    if (t < kClasses) sc[t] = 0;
+    if (t < kXcd * kClasses) sc[t / kClasses][t % kClasses] = 0;
     __syncthreads();
     const int c = order_class(cls, i, B);
     #pragma unroll
     for (int k = 0; k < kClasses; ++k) {
         const uint64_t m = __ballot(c == k);
-        if ((t & 63) == 0 && m) atomicAdd(&sc[k], __popcll(m));
-    }
-    __syncthreads();
-    if (t < kClasses) cnt[blockIdx.x * kClasses + t] = sc[t];
-}
-
-// pass 2: position = (lanes of lower classes) + (class-c lanes of earlier blocks)
-// + (class-c lanes earlier in this block)
-__global__ __launch_bounds__(1024) void k_order_scatter(const uint8_t* cls, const int32_t* cnt, int32_t* perm, int B,
-                                                        int nblk) {
-    __shared__ int tot[kClasses], pre[kClasses], wsum[16][kClasses];
-    const int t = threadIdx.x, b = blockIdx.x, w = t >> 6, l = t & 63;
-    if (t < kClasses) { tot[t] = 0; pre[t] = 0; }
-    __syncthreads();
-    int a_tot[kClasses], a_pre[kClasses];
-    #pragma unroll
-    for (int k = 0; k < kClasses; ++k) { a_tot[k] = 0; a_pre[k] = 0; }
-    for (int j = t; j < nblk; j += 1024) {
-        #pragma unroll
-        for (int k = 0; k < kClasses; ++k) {
-            const int v = cnt[j * kClasses + k];
-            a_tot[k] += v;
-            a_pre[k] += j < b ? v : 0;
+        if (xcd) {
+            // the wave's four 16-lane runs belong to sub-lists (4w + s) & 7
+            if ((t & 63) < 4) {
+                const int s = t & 3;
+                const int n = __popcll(m & (0xFFFFull << (16 * s)));
+                if (n) atomicAdd(&sc[(4 * w + s) & 7][k], n);
+            }
+        } else if ((t & 63) == 0 && m) {
+            atomicAdd(&sc[0][k], __popcll(m));
         }
     }
-    #pragma unroll
-    for (int k = 0; k < kClasses; ++k) {
-        if (a_tot[k]) atomicAdd(&tot[k], a_tot[k]);
-        if (a_pre[k]) atomicAdd(&pre[k], a_pre[k]);
+    __syncthreads();
+    if (t < kXcd * kClasses) cnt[blockIdx.x * kXcd * kClasses + t] = sc[t / kClasses][t % kClasses];
+}
+
+// pass 2: position (within the lane's sub-list) = (lanes of lower classes) +
+// (class-c lanes of earlier blocks) + (class-c lanes earlier in this block)
+__global__ __launch_bounds__(1024) void k_order_scatter(const uint8_t* cls, const int32_t* cnt, int32_t* perm, int B,
+                                                        int nblk, int xcd) {
+    constexpr int NC = kXcd * kClasses;
+    __shared__ int tot[NC], pre[NC], wsum[16][4][kClasses];
+    const int t = threadIdx.x, b = blockIdx.x, w = t >> 6, l = t & 63;
+    if (t < NC) { tot[t] = 0; pre[t] = 0; }
+    __syncthreads();
+    // thread t < NC sums counter t over the blocks (40 counters, <= B/1024 blocks)
+    if (t < NC) {
+        int a_tot = 0, a_pre = 0;
+        for (int j = 0; j < nblk; ++j) {
+            const int v = cnt[j * NC + t];
+            a_tot += v;
+            a_pre += j < b ? v : 0;
+        }
+        tot[t] = a_tot;
+        pre[t] = a_pre;
     }
     const int i = b * 1024 + t;
     const int c = order_class(cls, i, B);
+    const int s = xcd ? (l >> 4) : 0;                 // the lane's 16-lane run within the wave
+    const uint64_t seg = xcd ? (0xFFFFull << (16 * s)) : ~0ull;
     int rank = 0;
     #pragma unroll
     for (int k = 0; k < kClasses; ++k) {
         const uint64_t m = __ballot(c == k);
-        if (c == k) rank = __popcll(m & ((1ull << l) - 1ull));
-        if (l == 0) wsum[w][k] = __popcll(m);
+        if (c == k) rank = __popcll(m & seg & ((1ull << l) - 1ull));
+        if (l < 4) wsum[w][l][k] = __popcll(m & (xcd ? (0xFFFFull << (16 * l)) : (l == 0 ? ~0ull : 0ull)));
     }
     __syncthreads();
     if (c < kClasses) {
-        int pos = pre[c] + rank;
-        for (int k = 0; k < c; ++k) pos += tot[k];
-        for (int v = 0; v < w; ++v) pos += wsum[v][c];
-        perm[pos] = i;
+        const int x = xcd ? ((4 * w + s) & 7) : 0;
+        int pos = pre[x * kClasses + c] + rank;
+        for (int k = 0; k < c; ++k) pos += tot[x * kClasses + k];
+        // earlier waves of this block holding runs of the same sub-list: w' = w (mod 2)
+        for (int v = xcd ? (w & 1) : 0; v < w; v += xcd ? 2 : 1) pos += wsum[v][s][c];
+        perm[xcd ? pos * kXcd + x : pos] = i;
     }
 }
 
@@ -390,9 +411,10 @@ int bgx_internal_fail(hipError_t e) { return fail(e); }
 static void launch_order(bgx_engine* e, hipStream_t s) {
     const int nblk = (e->a.B + 1023) / 1024;
     hipLaunchKernelGGL(k_order_count, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->a.B,
-                       e->ovf_base + 4 * (e->ovf_parity ^ 1));
+                       e->ovf_base + 4 * (e->ovf_parity ^ 1), e->a.xcd);
     e->ovf_next_zeroed = true;
-    hipLaunchKernelGGL(k_order_scatter, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->perm, e->a.B, nblk);
+    hipLaunchKernelGGL(k_order_scatter, dim3(nblk), dim3(1024), 0, s, e->a.cls, e->order_cnt, e->perm, e->a.B, nblk,
+                       e->a.xcd);
     e->perm_valid = true;
 }
 
@@ -415,10 +437,14 @@ static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, c
 // Doubles share of the dispatch order (Philox mode): the expected doubles
 // fraction 1/6 plus 4 sigma.  Lanes past it run in the light launch whatever
 // their class (exact either way; an unpredicted doubles lane is only slower).
-static int heavy_grid(int B) {
+// With the XCD-aware order the count is a multiple of 8, so the light launch's
+// blocks keep the order's position -> XCD residue.
+static int heavy_grid(int B, bool xcd) {
     const char* f = getenv("BGX_HEAVY_FRAC");
     const double g = f ? atof(f) * B : B / 6.0 + 4.0 * std::sqrt(B * 5.0 / 36.0) + 32.0;
-    return g >= B ? B : (int)g;
+    int h = g >= B ? B : (int)g;
+    if (xcd) h = (h + 7) & ~7;
+    return h > B ? B : h;
 }
 
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
@@ -462,6 +488,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
     A.key0 = (uint32_t)seed; A.key1 = (uint32_t)(seed >> 32);
+    const char* xc = getenv("BGX_XCD");
+    A.xcd = batch % 128 == 0 && !(xc && xc[0] == '0') ? 1 : 0;
     e->slow_waves = kSlowWaves;
     const size_t B = (size_t)batch;
     hipError_t err = hipSuccess;
@@ -482,7 +510,7 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     if (dice_mode == BGX_DICE_PHILOX && !(so && so[0] == '0')) {
         alloc((void**)&e->perm, B * 4);
         alloc((void**)&A.cls, B);
-        alloc((void**)&e->order_cnt, (B / 1024 + 1) * kClasses * 4);
+        alloc((void**)&e->order_cnt, (B / 1024 + 1) * kXcd * kClasses * 4);
     }
     if (err != hipSuccess) { bgx_engine_destroy(e); return fail(err, BGX_ENOMEM); }
     if (hipMemset(A.lanes, 0, B * 64) != hipSuccess || hipMemset(A.ctr, 0, B * 8) != hipSuccess ||
@@ -627,7 +655,7 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     } else {
         Args a = A;
         a.perm = e->perm_valid ? e->perm : nullptr;
-        const int heavy = a.perm && e->split ? heavy_grid(A.B) : A.B;
+        const int heavy = a.perm && e->split ? heavy_grid(A.B, A.xcd != 0) : A.B;
         // Split dispatch (Philox mode): the predicted-doubles prefix of the order
         // with the big dedup table + revisit memo (26 KB of LDS per wave), then the
         // rest with a 256-slot table, no memo, no doubles code (4 KB, 49 VGPRs: the

@@ -253,3 +253,40 @@ def test_philox_split_dispatch_vs_oracle(bgx):
                     assert np.array_equal(rec[i, :52].view(np.int8), after), (t, i)
     assert checked_dbl > 500
     assert eng.error() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [16384, 1000])
+def test_dispatch_order_does_not_change_results(bgx, monkeypatch, B):
+    """The dispatch order (class-sorted, XCD-aware 16-lane runs when B % 128 == 0,
+    plain class sort otherwise, or no order at all with the run swizzle) only
+    schedules: every variant must step every lane exactly once and give the same
+    records, move lists and rewards."""
+    variants = [{}, {"BGX_XCD": "0"}, {"BGX_ORDER": "0"}, {"BGX_ORDER": "0", "BGX_XCD": "0"}]
+    engs = []
+    for env in variants:
+        for k in ("BGX_XCD", "BGX_ORDER"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        e = bgx.Engine(batch=B, max_moves=500, dice="philox", seed=21, auto_reset=True)
+        e.reset(want_obs=False)
+        engs.append(e)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for _ in range(30):
+        u = torch.rand(B, device="cuda", generator=g)
+        outs = []
+        for e in engs:
+            a = (u * e.n_moves().clamp(min=1).float()).to(torch.int32)
+            _, r, d, _ = e.step(a, want_obs=False)
+            outs.append((r.clone(), d.clone()))
+        for r, d in outs[1:]:
+            assert torch.equal(r, outs[0][0]) and torch.equal(d, outs[0][1])
+    rec0, mv0, nt0 = engs[0].lanes()
+    n0 = (rec0[:, 60].long() | (rec0[:, 61].long() << 8))
+    live = torch.arange(500, device="cuda")[None, :] < n0[:, None]     # entries past n are scratch
+    for e in engs[1:]:
+        rec, mv, nt = e.lanes()
+        assert torch.equal(rec, rec0) and torch.equal(nt, nt0)
+        assert torch.equal(torch.where(live, mv, 0), torch.where(live, mv0, 0))
+        assert e.error() == 0

@@ -1,7 +1,15 @@
 """Summarize a tools/profile.sh run: per-kernel stats + HBM traffic per launch of
-the dominant kernels.  Traffic follows MI355X_MICROARCH.md §HBM: bytes =
-(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (FETCH_SIZE in KiB reads half of a wide
-coalesced stream on gfx950; the doubling is the guide's correction)."""
+the dominant kernels.
+
+FETCH_SIZE calibration (MI355X_MICROARCH.md §HBM: the guide's x2 correction is
+for 16-B-per-lane streaming reads; "other access widths are uncalibrated:
+calibrate on a known byte count in your own access pattern"):
+tools/calib/fetch_calib.hip -> profiles/r2_fetch_calibration.json.  The env
+step's access shapes -- a 64-B lane record read 1 B per lane, 4-/8-B scalar
+reads, 4-/8-B and 64-B stores -- are each ONE 64-B EA request that FETCH_SIZE
+tallies at 64 B, so the env-step kernels' bytes are (FETCH_SIZE + WRITE_SIZE)
+x 1024, not doubled; the 2-ply evaluator's 16-B-per-lane pool stream keeps the
+guide's doubling."""
 import csv
 import json
 import os
@@ -34,7 +42,7 @@ for s in stats:
     if f and w:
         k["FETCH_SIZE_KiB"] = statistics.mean(f)
         k["WRITE_SIZE_KiB"] = statistics.mean(w)
-        k["hbm_bytes_per_launch"] = (2 * k["FETCH_SIZE_KiB"] + k["WRITE_SIZE_KiB"]) * 1024
+        k["hbm_bytes_per_launch"] = (k["FETCH_SIZE_KiB"] + k["WRITE_SIZE_KiB"]) * 1024   # calibrated, see top
     kernels.append(k)
 # per-dispatch durations of the dominant kernels over the timed tail (last --steps launches)
 tail = None
