@@ -58,6 +58,42 @@ def lane_returns(rewards: torch.Tensor, dones: torch.Tensor, gamma: float = GAMM
     return out
 
 
+EPISODE_STATS = ("episodes", "episode_reward_sum", "wins", "p1_wins", "gammons", "backgammons")
+
+
+def episode_stats(rewards: torch.Tensor, dones: torch.Tensor, movers: torch.Tensor,
+                  carry: torch.Tensor) -> torch.Tensor:
+    """The reference loop's per-env episode accounting (train.py:55-99) over a
+    [T, B] rollout, on the device without a per-step loop.
+
+    `carry` [B] (fp64) is each lane's reward accumulated in its unfinished
+    episode (`episode_rewards`, train.py:58) and is updated in place.  Returns
+    the sums named by EPISODE_STATS as one fp64 tensor: finished episodes,
+    their summed episode rewards (train.py:73), wins as the reference counts
+    them (`info["winner"] == info["current_player"]`, train.py:74-77: the
+    mover of a winning step, i.e. a done with a positive reward), wins by
+    PLAYER1 (`log_metrics`' "1 if Player1 wins", ppo_agent.py:494), and
+    gammon / backgammon wins (rewards 1.5 / 2.0, backgammon_env.py:26-28).
+    `movers` [T, B] is the player to move before each step (record byte 52).
+    """
+    T, B = rewards.shape
+    d = dones.bool()
+    r = rewards.double()
+    seg = torch.cumsum(d, 0, dtype=torch.int64) - d.long()      # episodes finished before step t
+    idx = seg + torch.arange(B, device=r.device, dtype=torch.int64) * (T + 1)
+    sums = torch.zeros(B * (T + 1), dtype=torch.float64, device=r.device)
+    sums.scatter_add_(0, idx.reshape(-1), r.reshape(-1))
+    sums = sums.view(B, T + 1)
+    sums[:, 0] += carry
+    n = d.sum(0, dtype=torch.int64)
+    open_ep = sums.gather(1, n[:, None]).squeeze(1)
+    finished = sums.sum(1) - open_ep
+    carry.copy_(open_ep)
+    return torch.stack([n.sum().double(), finished.sum(),
+                        (d & (r > 0)).sum().double(), (d & (r > 0) & (movers == 0)).sum().double(),
+                        (d & (r == 1.5)).sum().double(), (d & (r == 2.0)).sum().double()])
+
+
 def reference_returns(rewards: torch.Tensor, dones: torch.Tensor, gamma: float = GAMMA) -> torch.Tensor:
     """ppo_agent.py:206-216 over the flat step-major memory (envs interleaved)."""
     flat_r = rewards.reshape(-1).double().cpu().numpy()
@@ -305,6 +341,8 @@ class PPOTrainer:
         if pinned:
             self.pinned = {k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in self.buf.items()}
             self.copy_stream = torch.cuda.Stream(self.dev)
+        self.ep_carry = torch.zeros(B, dtype=torch.float64, **kw)     # train.py:58 episode_rewards
+        self.last_episode_stats = None
         self.eng.reset(want_obs=False)
 
     def rollout(self):
@@ -323,11 +361,11 @@ class PPOTrainer:
                 with torch.cuda.stream(self.copy_stream):
                     for k in buf:
                         self.pinned[k][t].copy_(buf[k][t], non_blocking=True)
-        eps = int(buf["dones"].sum().item())
+        st = episode_stats(buf["rewards"], buf["dones"], buf["records"][:, :, 52], self.ep_carry)
         if _world(self.group) > 1:
-            e = torch.tensor([eps], device=self.dev)
-            dist.all_reduce(e, group=self.group)
-            eps = int(e.item())
+            dist.all_reduce(st, group=self.group)
+        self.last_episode_stats = dict(zip(EPISODE_STATS, st.tolist()))
+        eps = int(self.last_episode_stats["episodes"])
         self.total_episodes += eps
         return eps
 
@@ -384,6 +422,11 @@ class PPOTrainer:
         torch.cuda.synchronize(self.dev)
         t2 = time.perf_counter()
         ws = _world(self.group)
+        e = self.last_episode_stats
+        k = max(e["episodes"], 1.0)
+        m.update({"avg_episode_reward": e["episode_reward_sum"] / k, "win_rate": e["wins"] / k,
+                  "p1_win_rate": e["p1_wins"] / k, "gammon_rate": e["gammons"] / k,
+                  "backgammon_rate": e["backgammons"] / k, "total_episodes": self.total_episodes})
         m.update({"episodes": eps, "env_steps": self.B * self.T * ws, "rollout_s": t1 - t0, "update_s": t2 - t1,
                   "env_steps_per_s": self.B * self.T * ws / (t2 - t0), "entropy_coef": self.entropy_coef})
         return m

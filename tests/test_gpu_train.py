@@ -27,6 +27,15 @@ def test_trainer_iteration():
     assert bool((r[~d] == 0).all()) and bool(torch.isin(r[d], torch.tensor([1.0, 1.5, 2.0], device="cuda")).all())
     m2 = tr.iteration()
     assert np.isfinite(m2["total_loss"])
+    # episode metrics (train.py:64-99): every finished self-play episode is a win for
+    # its last mover, and its reward is that win's reward (no other rewards occur)
+    for _ in range(16):
+        m3 = tr.iteration()
+        if m3["episodes"] > 0:
+            break
+    assert m3["episodes"] > 0 and m3["win_rate"] == 1.0
+    assert 0.0 <= m3["p1_win_rate"] <= 1.0 and 1.0 <= m3["avg_episode_reward"] <= 2.0
+    assert m3["total_episodes"] == tr.total_episodes
 
 
 def test_reference_returns_mode():

@@ -210,3 +210,36 @@ def test_two_rank_global_normalize_large():
     full = ((R - R.mean()) / (R.std() + 1e-5)).numpy()
     got = np.concatenate([res[0], res[1]])
     assert np.abs(got - full).max() < 1e-6
+
+
+def test_episode_stats_match_reference_loop():
+    """bgx.train.episode_stats == the reference loop's per-env accounting
+    (train.py:55-99: episode_rewards += rewards; on done record the episode
+    reward and win = winner == current_player, then zero), carried across two
+    rollouts."""
+    from bgx.train import episode_stats, EPISODE_STATS
+    g = torch.Generator().manual_seed(3)
+    T, B = 16, 37
+    carry = torch.zeros(B, dtype=torch.float64)
+    ref_acc = [0.0] * B
+    for _ in range(2):
+        dones = (torch.rand(T, B, generator=g) < 0.15).to(torch.uint8)
+        win_r = torch.tensor([1.0, 1.5, 2.0])[torch.randint(0, 3, (T, B), generator=g)]
+        rewards = torch.where(dones.bool(), win_r, torch.randint(0, 2, (T, B), generator=g) * 0.01)
+        movers = torch.randint(0, 2, (T, B), generator=g, dtype=torch.uint8)
+        got = dict(zip(EPISODE_STATS, episode_stats(rewards, dones, movers, carry).tolist()))
+        want = dict.fromkeys(EPISODE_STATS, 0.0)
+        for t in range(T):
+            for i in range(B):
+                ref_acc[i] += float(rewards[t, i])
+                if dones[t, i]:
+                    want["episodes"] += 1
+                    want["episode_reward_sum"] += ref_acc[i]
+                    want["wins"] += 1                       # winner == current_player on every win step
+                    want["p1_wins"] += int(movers[t, i] == 0)
+                    want["gammons"] += int(rewards[t, i] == 1.5)
+                    want["backgammons"] += int(rewards[t, i] == 2.0)
+                    ref_acc[i] = 0.0
+        for k in EPISODE_STATS:
+            assert got[k] == pytest.approx(want[k], abs=1e-9), k
+        np.testing.assert_allclose(carry.numpy(), np.array(ref_acc), atol=1e-12)
