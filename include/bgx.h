@@ -100,6 +100,13 @@ int bgx_movegen(bgx_engine* e, const int8_t* boards52_dev, const uint8_t* player
  * get_board_features_batch_from_tensors (ai/batching.py:78-147). */
 int bgx_encode(const int8_t* boards52_dev, const uint8_t* players_dev, int32_t n, float* out_dev, void* stream);
 
+/* The same 198 features from n 64-byte lane records (records_dev: n x 64 bytes,
+ * board bytes 0..51, player to move at byte 52 -- the rollout rows the PPO update
+ * re-encodes, ppo_agent.py:221-229 / 274 stacks the stored observations and casts
+ * them under autocast).  dtype 0: fp32 [n][198]; 1: fp16 [n][198], the round to
+ * nearest of the fp32 features (autocast's cast). */
+int bgx_encode_records(const uint8_t* records_dev, int32_t n, int32_t dtype, void* out_dev, void* stream);
+
 /* execute_full_move_on_board_copy (immutable_board.py:224-233) over every legal
  * move of lanes [lane0, lane0+nlanes): boards52 int8[nlanes][max_moves][52]
  * (rows past n_moves are zero). */
@@ -216,6 +223,14 @@ int bgx_ppo_head_ex(const void* logits_dev, int32_t dtype, int64_t ld_logits, co
                     const float* returns_dev, const float* adv_dev, int32_t n, int32_t n_actions, float eps_clip,
                     float c_value, float c_entropy, float grad_scale, void* dlogits_dev, int64_t ld_dlogits,
                     void* dvalues_dev, double* sums_dev, int32_t pad_value_col, float* colsum_dev, void* stream);
+
+/* The fp16 epoch's ReLU backward of fc1 (policy_network.py:70; autograd passes the
+ * gradient where relu's output > 0) in place on dh [n][hidden] fp16, given the
+ * stored activations h [n][hidden] fp16 (16-byte aligned, hidden % 8 == 0,
+ * hidden <= 256), with the bias gradient's partial column sums of the masked dh
+ * in colsum[blocks][hidden] (fp32; the caller sums the rows). */
+int bgx_relu_backward(void* dh, const void* h, int32_t n, int32_t hidden, float* colsum, int32_t blocks,
+                      void* stream);
 
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf

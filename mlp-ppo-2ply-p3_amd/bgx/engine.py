@@ -212,6 +212,22 @@ class Engine:
         return nm, nt, mv
 
 
+def encode_records(records: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    """get_board_features of n 64-byte lane records (board bytes 0..51, player to
+    move at 52) as fp32, or fp16 = the fp32 features rounded (autocast's cast)."""
+    if records.dim() != 2 or records.shape[1] != 64 or records.element_size() != 1:
+        raise ValueError(f"encode_records: records must be [n, 64] bytes, got {tuple(records.shape)} {records.dtype}")
+    if dtype not in (torch.float32, torch.float16):
+        raise ValueError(f"encode_records: dtype must be float32 or float16, got {dtype}")
+    L = _lib.load()
+    r = records.contiguous()
+    out = torch.empty(r.shape[0], 198, dtype=dtype, device=r.device)
+    s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
+    check(L.bgx_encode_records(_ptr(r), r.shape[0], 0 if dtype == torch.float32 else 1, _ptr(out), s),
+          "bgx_encode_records")
+    return out
+
+
 def encode(boards52: torch.Tensor, players: torch.Tensor) -> torch.Tensor:
     """ImmutableBoard.get_board_features for a batch (immutable_board.py:171-212)."""
     L = _lib.load()

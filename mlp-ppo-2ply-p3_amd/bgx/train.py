@@ -40,7 +40,7 @@ import ctypes
 
 from . import _lib
 from ._lib import check
-from .engine import Engine, encode
+from .engine import Engine, encode_records
 from .policy import PolicyNet, MASK_LOG
 from .ppo import (EPS_CLIP, GAMMA, LEARNING_RATE, NUM_EPOCHS, VALUE_LOSS_COEF, ENTROPY_COEF_START,
                   ENTROPY_COEF_END, ENTROPY_ANNEAL_EPISODES, allreduce_mean_, global_normalize, _world)
@@ -109,7 +109,7 @@ def reference_returns(rewards: torch.Tensor, dones: torch.Tensor, gamma: float =
 
 
 def features_and_masks(records: torch.Tensor, n_actions: int):
-    feats = encode(records[:, :52].contiguous(), records[:, 52].contiguous())
+    feats = encode_records(records)
     counts = records[:, 60].to(torch.int32) | (records[:, 61].to(torch.int32) << 8)
     legal = torch.arange(n_actions, device=records.device)[None, :] < counts[:, None]
     return feats, legal
@@ -118,7 +118,8 @@ def features_and_masks(records: torch.Tensor, n_actions: int):
 def _is_policy_mlp(net) -> bool:
     """The manual fp16 epoch needs exactly relu(fc1) -> {action_head, value_head}."""
     return (isinstance(net, PolicyNet) and type(net).forward is PolicyNet.forward
-            and all(getattr(net, k).bias is not None for k in ("fc1", "action_head", "value_head")))
+            and all(getattr(net, k).bias is not None for k in ("fc1", "action_head", "value_head"))
+            and net.fc1.out_features % 8 == 0 and net.fc1.out_features <= 256)     # bgx_relu_backward
 
 
 class _PPOHead(torch.autograd.Function):
@@ -195,6 +196,7 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
 
 
 PPO_COLSUM_BLOCKS = 2048       # include/bgx.h BGX_PPO_COLSUM_BLOCKS
+RELU_BLOCKS = 1024             # bgx_relu_backward's grid (rows of its column-sum partials)
 
 
 def _wgrad(g: torch.Tensor, x: torch.Tensor, splits: int = 64) -> torch.Tensor:
@@ -247,6 +249,7 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
         p = lambda t: ctypes.c_void_p(t.data_ptr())
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         colsum = torch.empty(PPO_COLSUM_BLOCKS, 512, dtype=torch.float32, device=dev)
+        hsum = torch.empty(RELU_BLOCKS, Hd, dtype=torch.float32, device=dev)
         for feats, legal, actions, old_logp, returns, adv, records in chunks:
             x = feats.half()
             h = torch.relu(F.linear(x, W1h, b1h))
@@ -264,9 +267,10 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
             gW2 += _wgrad(dy, h)
             gb2 += colsum.sum(0)[:Ap]
             dh = dy @ W2h
-            dh.masked_fill_(h <= 0, 0)                     # relu backward (grad where out > 0)
+            # relu backward (grad where out > 0) in place + the bias gradient's column sums
+            check(L.bgx_relu_backward(p(dh), p(h), m, Hd, p(hsum), RELU_BLOCKS, stream), "bgx_relu_backward")
             gW1 += _wgrad(dh, x)
-            gb1 += dh.sum(0, dtype=torch.float32)
+            gb1 += hsum.sum(0)
         if post != 1.0:
             for t in (gW1, gb1, gW2, gb2):
                 t.mul_(post)
@@ -398,7 +402,8 @@ class PPOTrainer:
             for s in range(0, N, self.chunk):
                 e = min(N, s + self.chunk)
                 if self.fused:      # the loss kernel reads the legal counts from the records
-                    f = encode(recs[s:e, :52].contiguous(), recs[s:e, 52].contiguous())
+                    # under autocast the GEMMs take fp16 features: encode straight to fp16
+                    f = encode_records(recs[s:e], torch.float16 if self.amp else torch.float32)
                     legal = None
                 else:
                     f, legal = features_and_masks(recs[s:e], self.A)

@@ -298,6 +298,51 @@ __global__ __launch_bounds__(64) void k_encode(const int8_t* boards, const uint8
     }
 }
 
+// Feature f of the 64-byte record `rec` (board bytes 0..51, player to move at 52),
+// as feature_at (immutable_board.py:171-212).
+__device__ __forceinline__ float rec_feature(const uint8_t* rec, int f) {
+    if (f >= 196) return (f == 196) == (rec[R_CUR] == 0) ? 1.0f : 0.0f;
+    const int p = f >= 98 ? 1 : 0;
+    const int g = f - 98 * p;
+    if (g < 96) {
+        const int n = rec[p * 24 + (g >> 2)], u = g & 3;
+        if (u < 3) return n >= u + 1 ? 1.0f : 0.0f;
+        return n >= 3 ? (float)(n - 3) * 0.5f : 0.0f;
+    }
+    if (g == 96) return (float)rec[48 + p] * 0.5f;
+    return kOff15[rec[50 + p] & 15];
+}
+
+// The 198 features of n 64-byte lane records (the rollout's stored records), as
+// T = float or _Float16 (fp16: the rounding of the fp32 features that autocast's
+// cast applies, ppo_agent.py:274).  A 256-thread block stages 64 records in LDS
+// (one 16-byte load per thread) and writes their 64 x 198 outputs as contiguous
+// feature pairs (coalesced stores).
+template <typename T>
+__global__ __launch_bounds__(256) void k_encode_rec(const uint8_t* __restrict__ records, int n, T* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t rec[64 * 64];
+    for (int r0 = blockIdx.x * 64; r0 < n; r0 += gridDim.x * 64) {
+        const int nr = min(64, n - r0);
+        __syncthreads();
+        if ((int)threadIdx.x < nr * 4)
+            ((uint4*)rec)[threadIdx.x] = ((const uint4*)(records + (size_t)r0 * 64))[threadIdx.x];
+        __syncthreads();
+        for (int q = threadIdx.x; q < nr * 99; q += blockDim.x) {
+            const int row = q / 99, f = 2 * (q - row * 99);
+            const uint8_t* rr = rec + row * 64;
+            const float a = rec_feature(rr, f), b = rec_feature(rr, f + 1);
+            T* o = out + (size_t)(r0 + row) * 198 + f;
+            if (sizeof(T) == 2) {
+                typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+                h2 v; v[0] = (_Float16)a; v[1] = (_Float16)b;
+                *(h2*)o = v;
+            } else {
+                *(float2*)o = make_float2(a, b);
+            }
+        }
+    }
+}
+
 // Afterstates / afterstate features of every legal move of a lane.
 // MODE 0: int8 boards [M][52]; MODE 1: float features [M][198] (mover one-hot).
 template <int MODE>
@@ -424,6 +469,8 @@ static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, c
     if (e->memo_mode == 2) {
         if (e->lds_log == 11)
             hipLaunchKernelGGL((k_step<0, 11, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
+        else if (e->lds_log == 9)
+            hipLaunchKernelGGL((k_step<0, 9, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
         else
             hipLaunchKernelGGL((k_step<0, 10, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
     } else if (e->lds_log == 9)
@@ -712,6 +759,20 @@ int bgx_encode(const int8_t* boards52_dev, const uint8_t* players_dev, int32_t n
     if (n < 0 || (n > 0 && (!boards52_dev || !players_dev || !out_dev))) return BGX_EINVAL;
     if (n == 0) return BGX_OK;
     hipLaunchKernelGGL(k_encode, dim3(n), dim3(64), 0, (hipStream_t)stream, boards52_dev, players_dev, n, out_dev);
+    CKL();
+    return BGX_OK;
+}
+
+int bgx_encode_records(const uint8_t* records_dev, int32_t n, int32_t dtype, void* out_dev, void* stream) {
+    if (n < 0 || (dtype != 0 && dtype != 1) || (n > 0 && (!records_dev || !out_dev))) return BGX_EINVAL;
+    if (n == 0) return BGX_OK;
+    const int blocks = (n + 63) / 64 < 8192 ? (n + 63) / 64 : 8192;
+    if (dtype == 0)
+        hipLaunchKernelGGL(k_encode_rec<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, records_dev, n,
+                           (float*)out_dev);
+    else
+        hipLaunchKernelGGL(k_encode_rec<_Float16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, records_dev, n,
+                           (_Float16*)out_dev);
     CKL();
     return BGX_OK;
 }

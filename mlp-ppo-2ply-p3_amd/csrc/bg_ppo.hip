@@ -6,9 +6,10 @@
 // clamp(): inclusive bounds pass it).  Replaces ~20 elementwise / softmax passes
 // over the [n, A] logits (forward and backward) with one read and one write.
 //
-// One wave per row (A <= 512: 8 consecutive columns per lane, two 8-byte fp16 /
-// 16-byte fp32 accesses when the rows are aligned), rows grid-strided; the loss
-// sums go to three double accumulators (one atomic each per workgroup).
+// Two rows per wave (A <= 512: 16 consecutive columns per lane of a 32-lane half,
+// four 8-byte fp16 / 16-byte fp32 accesses when the rows are aligned), rows
+// grid-strided; the loss sums go to three double accumulators (one atomic each per
+// workgroup).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
@@ -24,49 +25,70 @@ constexpr float kLogEps = -15.942384719848633f;
 constexpr float kLog1mEps = -1.1920930376163597e-07f;
 
 
-__device__ __forceinline__ float wave_max(float v) {
-    #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+// Reductions over a 32-lane half-wave: DPP row_ror 8/4/2/1 inside each 16-lane row,
+// then ds_swizzle xor 16 (32-lane bitmask mode) across the two rows; every lane of
+// the half gets the result.
+template <int CTRL>
+__device__ __forceinline__ float dpp_ror(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float wave_sum(float v) {
-    #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+__device__ __forceinline__ float swz_x16(float v) {
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));   // and 0x1f, xor 0x10
 }
+#define BGX_HALF_REDUCE(OP, v)                \
+    do {                                     \
+        v = OP(v, dpp_ror<0x128>(v));        \
+        v = OP(v, dpp_ror<0x124>(v));        \
+        v = OP(v, dpp_ror<0x122>(v));        \
+        v = OP(v, dpp_ror<0x121>(v));        \
+        v = OP(v, swz_x16(v));               \
+    } while (0)
+__device__ __forceinline__ float fadd(float a, float b) { return a + b; }
 
-// 8 consecutive columns per lane as one 16-byte (fp16) / two 16-byte (fp32) access
-template <typename T> struct Vec8;
-template <> struct Vec8<_Float16> {          // two 8-byte halves (a 500-wide fp16 row is 8-byte aligned)
+// 16 consecutive columns per lane: 8-byte (fp16: 4 columns) / 16-byte (fp32: 4) accesses
+template <typename T> struct Vec16;
+template <> struct Vec16<_Float16> {
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    static constexpr int kAlign = 8;
     static __device__ __forceinline__ void load(const _Float16* p, float* z) {
-        const h4 a = ((const h4*)p)[0], b = ((const h4*)p)[1];
+        h4 a[4];
         #pragma unroll
-        for (int i = 0; i < 4; ++i) { z[i] = (float)a[i]; z[4 + i] = (float)b[i]; }
+        for (int k = 0; k < 4; ++k) a[k] = ((const h4*)p)[k];
+        #pragma unroll
+        for (int k = 0; k < 4; ++k)
+            #pragma unroll
+            for (int i = 0; i < 4; ++i) z[4 * k + i] = (float)a[k][i];
     }
     static __device__ __forceinline__ void store(_Float16* p, const float* g) {
-        h4 a, b;
         #pragma unroll
-        for (int i = 0; i < 4; ++i) { a[i] = (_Float16)g[i]; b[i] = (_Float16)g[4 + i]; }
-        ((h4*)p)[0] = a;
-        ((h4*)p)[1] = b;
+        for (int k = 0; k < 4; ++k) {
+            h4 a;
+            #pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = (_Float16)g[4 * k + i];
+            ((h4*)p)[k] = a;
+        }
     }
 };
-template <> struct Vec8<float> {
-    static constexpr int kAlign = 16;
+template <> struct Vec16<float> {
     static __device__ __forceinline__ void load(const float* p, float* z) {
-        const float4 a = ((const float4*)p)[0], b = ((const float4*)p)[1];
-        z[0] = a.x; z[1] = a.y; z[2] = a.z; z[3] = a.w; z[4] = b.x; z[5] = b.y; z[6] = b.z; z[7] = b.w;
+        float4 a[4];
+        #pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = ((const float4*)p)[k];
+        #pragma unroll
+        for (int k = 0; k < 4; ++k) { z[4 * k] = a[k].x; z[4 * k + 1] = a[k].y; z[4 * k + 2] = a[k].z; z[4 * k + 3] = a[k].w; }
     }
     static __device__ __forceinline__ void store(float* p, const float* g) {
-        ((float4*)p)[0] = make_float4(g[0], g[1], g[2], g[3]);
-        ((float4*)p)[1] = make_float4(g[4], g[5], g[6], g[7]);
+        #pragma unroll
+        for (int k = 0; k < 4; ++k) ((float4*)p)[k] = make_float4(g[4 * k], g[4 * k + 1], g[4 * k + 2], g[4 * k + 3]);
     }
 };
 
+// Two rows per wave, one per 32-lane half (lane l: row half l >> 5, columns
+// 16 (l & 31) .. +15): the row reductions are DPP rotations + one swizzle (no
+// LDS memory round trips), 16 columns per lane keep the registers at 4 waves
+// per SIMD, and the chosen action's logit is read directly (its log-prob needs
+// no per-column select).  Rows grid-strided over the halves.
 template <typename T>
-__global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, int64_t ld_logits,
+__global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logits, int64_t ld_logits,
                                                   const T* __restrict__ values, const uint8_t* __restrict__ records,
                                                   const int32_t* __restrict__ actions,
                                                   const float* __restrict__ old_logp,
@@ -75,61 +97,66 @@ __global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, 
                                                   float gscale, T* __restrict__ dlogits, int64_t ld_dlogits,
                                                   T* __restrict__ dvalues, double* __restrict__ sums, int vec,
                                                   int pad, float* __restrict__ colsum) {
+    constexpr int C = 16;
     const int l = threadIdx.x & 63;
-    const int nw = gridDim.x * (blockDim.x >> 6);
-    const int j0 = 8 * l;                      // this lane's columns j0 .. j0+7
-    double s_pol = 0.0, s_val = 0.0, s_ent = 0.0;
-    float cs[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};   // column sums of the stored gradient
-    for (int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < n; row += nw) {
+    const int c32 = l & 31;
+    const int nh = gridDim.x * (blockDim.x >> 5);          // 32-lane halves in the grid
+    const int j0 = C * c32;                                 // this lane's columns j0 .. j0+15
+    const bool vload = vec && j0 + C <= ld_logits;
+    const bool vstore = vec && j0 + C <= ld_dlogits && (pad || j0 + C <= A);
+    float s_pol = 0.0f, s_val = 0.0f, s_ent = 0.0f;      // per-half partials (<= a few hundred rows)
+    float cs[C];
+    #pragma unroll
+    for (int i = 0; i < C; ++i) cs[i] = 0.0f;
+    for (int row = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5); row < n; row += nh) {
         const T* lg = logits + (int64_t)row * ld_logits;
         const uint8_t* rec = records + (int64_t)row * 64;
         const int cnt = (int)rec[60] | ((int)rec[61] << 8);
-        float z[8];
-        if (vec && j0 + 8 <= A) {
-            Vec8<T>::load(lg + j0, z);
+        const int act = actions[row];
+        const float a = adv[row], olp = old_logp[row], ret = returns[row];
+        const float v = (float)values[row];
+        const float za = (float)lg[act] + (act < cnt ? 0.0f : kMaskLog);
+        float z[C];
+        if (vload) {
+            Vec16<T>::load(lg + j0, z);
         } else {
             #pragma unroll
-            for (int i = 0; i < 8; ++i) z[i] = j0 + i < A ? (float)lg[j0 + i] : 0.0f;
+            for (int i = 0; i < C; ++i) z[i] = j0 + i < A ? (float)lg[j0 + i] : 0.0f;
         }
         float m = -INFINITY;
         #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < C; ++i) {
             const int j = j0 + i;
             z[i] = j < A ? z[i] + (j < cnt ? 0.0f : kMaskLog) : -INFINITY;
             m = fmaxf(m, z[i]);
         }
-        m = wave_max(m);
-        float e[8], se = 0.0f;
+        BGX_HALF_REDUCE(fmaxf, m);
+        float se = 0.0f;
         #pragma unroll
-        for (int i = 0; i < 8; ++i) { e[i] = z[i] == -INFINITY ? 0.0f : __expf(z[i] - m); se += e[i]; }
-        se = wave_sum(se);
-        const float lse = m + __logf(se), inv = 1.0f / se;
+        for (int i = 0; i < C; ++i) se += __expf(z[i] - m);          // exp(-inf) = 0
+        BGX_HALF_REDUCE(fadd, se);
+        const float lse = m + __logf(se);
         // torch.distributions.Categorical(probs) semantics (ppo_agent.py:273-291):
         // log_prob and entropy use L = log(clamp(p, eps, 1 - eps)) (clamp_probs),
-        // whose gradient is zero outside [eps, 1 - eps]
-        float lp[8], inb[8], ent = 0.0f, s_in = 0.0f;
+        // whose gradient is zero outside [eps, 1 - eps].  z[i] <- p, q[i] <- L + in
+        float q[C], ent = 0.0f, s_in = 0.0f;
         #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < C; ++i) {
             const float u = z[i] - lse;
-            inb[i] = (u >= kLogEps && u <= kLog1mEps) ? 1.0f : 0.0f;
-            lp[i] = fminf(fmaxf(u, kLogEps), kLog1mEps);
-            e[i] *= inv;                           // p
-            ent -= z[i] == -INFINITY ? 0.0f : e[i] * lp[i];
-            s_in += e[i] * inb[i];
+            const float inb = (u >= kLogEps && u <= kLog1mEps) ? 1.0f : 0.0f;
+            const float lp = fminf(fmaxf(u, kLogEps), kLog1mEps);
+            const float pi = __expf(u);
+            z[i] = pi;
+            q[i] = lp + inb;
+            ent -= pi * lp;                        // p = 0 off the legal set (and past A)
+            s_in += pi * inb;
         }
-        ent = wave_sum(ent);
-        s_in = wave_sum(s_in);
-        const int act = actions[row];
-        float la = 0.0f, ina = 0.0f;
-        #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            la = (act & 7) == i ? lp[i] : la;
-            ina = (act & 7) == i ? inb[i] : ina;
-        }
-        const float nl = __shfl(la, (act >> 3) & 63);          // log pi(act), clamped
-        const float in_a = __shfl(ina, (act >> 3) & 63);
-        const float a = adv[row];
-        const float r = __expf(nl - old_logp[row]);
+        BGX_HALF_REDUCE(fadd, ent);
+        BGX_HALF_REDUCE(fadd, s_in);
+        const float ua = za - lse;
+        const float la = fminf(fmaxf(ua, kLogEps), kLog1mEps);          // log pi(act), clamped
+        const float ina = (ua >= kLogEps && ua <= kLog1mEps) ? 1.0f : 0.0f;
+        const float r = __expf(la - olp);
         const float s1 = r * a;
         const float rc = fminf(fmaxf(r, 1.0f - eps_clip), 1.0f + eps_clip);
         const float s2 = rc * a;
@@ -137,64 +164,103 @@ __global__ __launch_bounds__(256) void k_ppo_head(const T* __restrict__ logits, 
         // d(-min(s1, s2))/d logp: torch min() splits ties, clamp() passes inside [lo, hi]
         const float w1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
         const float w2 = (1.0f - w1) * ((r >= 1.0f - eps_clip && r <= 1.0f + eps_clip) ? 1.0f : 0.0f);
-        const float g_lp = -a * r * (w1 + w2) * in_a;
+        const float g_lp = -a * r * (w1 + w2) * ina;
         // d/dz_k of  -min(.) - c_e * H  with H = -sum L_j p_j:
         //   g_lp (d_ka - p_k) + c_e p_k (L_k + in_k + H - sum_j p_j in_j)
         const float ent_c = ent - s_in;
-        float g[8];
-        #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float pi = e[i];
-            g[i] = gscale * (g_lp * ((j0 + i == act ? 1.0f : 0.0f) - pi) + c_entropy * pi * (lp[i] + inb[i] + ent_c));
-        }
-        const float v = (float)values[row], dv = v - returns[row];
+        const float dv = v - ret;
         const float gv = gscale * c_value * 2.0f * dv;
+        float g[C];
+        #pragma unroll
+        for (int i = 0; i < C; ++i) {
+            const float pi = z[i];
+            const int j = j0 + i;
+            const float gj = gscale * (g_lp * ((j == act ? 1.0f : 0.0f) - pi) + c_entropy * pi * (q[i] + ent_c));
+            // with `pad`: column A = the value gradient and zeros up to ld_dlogits
+            // (the layout of a [logits | value | 0] GEMM)
+            g[i] = j < A ? gj : (j == A ? gv : 0.0f);
+        }
         T* dl = dlogits + (int64_t)row * ld_dlogits;
-        if (vec && j0 + 8 <= A) {
-            Vec8<T>::store(dl + j0, g);
+        if (vstore) {
+            Vec16<T>::store(dl + j0, g);
             #pragma unroll
-            for (int i = 0; i < 8; ++i) cs[i] += (float)(T)g[i];
+            for (int i = 0; i < C; ++i) cs[i] += (float)(T)g[i];
         } else {
-            // the row's tail; with `pad` also column A = the value gradient and
-            // zeros up to ld_dlogits (the layout of a [logits | value | 0] GEMM)
             #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < C; ++i) {
                 const int j = j0 + i;
-                const T t = j < A ? (T)g[i] : (j == A ? (T)gv : (T)0.0f);
                 if (j < A || (pad && j < ld_dlogits)) {
+                    const T t = (T)g[i];
                     dl[j] = t;
                     cs[i] += (float)t;
                 }
             }
         }
-        if (l == 0) {
+        if (c32 == 0) {
             dvalues[row] = (T)gv;
             s_pol += pol;
-            s_val += (double)dv * dv;
+            s_val += dv * dv;
             s_ent += ent;
         }
     }
     // one set of double atomics per workgroup (per-wave atomics on three addresses
     // serialised: measured 2.5 ms per 1M rows)
-    __shared__ double red[4][3];
-    const int w = threadIdx.x >> 6;
-    if (l == 0) { red[w][0] = s_pol; red[w][1] = s_val; red[w][2] = s_ent; }
+    __shared__ double red[8][3];
+    const int half = threadIdx.x >> 5;
+    if (c32 == 0) { red[half][0] = (double)s_pol; red[half][1] = (double)s_val; red[half][2] = (double)s_ent; }
     __syncthreads();
     if (threadIdx.x < 3) {
         double t = 0.0;
-        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i][threadIdx.x];
+        for (int i = 0; i < (int)(blockDim.x >> 5); ++i) t += red[i][threadIdx.x];
         atomicAdd(sums + threadIdx.x, t);
     }
     if (colsum) {                              // this workgroup's column sums -> colsum[block][512]
-        __shared__ float cred[4][512];
+        __shared__ float cred[8][512];
         #pragma unroll
-        for (int i = 0; i < 8; ++i) cred[w][j0 + i] = cs[i];
+        for (int i = 0; i < C; ++i) cred[half][j0 + i] = cs[i];
         __syncthreads();
         for (int c = threadIdx.x; c < 512; c += blockDim.x) {
             float t = 0.0f;
-            for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += cred[i][c];
+            for (int i = 0; i < (int)(blockDim.x >> 5); ++i) t += cred[i][c];
             colsum[(int64_t)blockIdx.x * 512 + c] = t;
         }
+    }
+}
+
+// ReLU backward of fc1 in place (torch.relu's gradient: passed where the output is
+// > 0, policy_network.py:70) fused with the bias gradient's column sums: dh, h fp16
+// [n][H] (H % 8 == 0, H <= 256), each thread 8 columns (one 16-byte access) of
+// a row; per-block column sums of the masked dh -> colsum[block][H] (fp32).
+__global__ __launch_bounds__(256) void k_relu_bwd(_Float16* __restrict__ dh, const _Float16* __restrict__ h, int n,
+                                                  int H, float* __restrict__ colsum) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const int tpr = H / 8;                          // threads per row
+    const int rows_per_it = blockDim.x / tpr;
+    const int t = threadIdx.x;
+    const int slot = t / tpr, c0 = 8 * (t - slot * tpr);
+    float cs[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (slot < rows_per_it) {
+        for (int row = blockIdx.x * rows_per_it + slot; row < n; row += gridDim.x * rows_per_it) {
+            h8* pd = (h8*)(dh + (int64_t)row * H + c0);
+            h8 d = *pd;
+            const h8 a = *(const h8*)(h + (int64_t)row * H + c0);
+            #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                d[i] = a[i] > (_Float16)0.0f ? d[i] : (_Float16)0.0f;
+                cs[i] += (float)d[i];
+            }
+            *pd = d;
+        }
+    }
+    __shared__ float red[256][9];
+    #pragma unroll
+    for (int i = 0; i < 8; ++i) red[t][i] = cs[i];
+    __syncthreads();
+    for (int c = t; c < H; c += blockDim.x) {
+        const int tc = c / 8, i = c - 8 * tc;
+        float acc = 0.0f;
+        for (int r = 0; r < rows_per_it; ++r) acc += red[r * tpr + tc][i];
+        colsum[(int64_t)blockIdx.x * H + c] = acc;
     }
 }
 
@@ -214,7 +280,7 @@ extern "C" int bgx_ppo_head_ex(const void* logits, int32_t dtype, int64_t ld_log
         return BGX_EINVAL;
     if (n == 0 && !colsum) return BGX_OK;
     // with column sums the grid is fixed (colsum is [kPpoColBlocks][512], every block writes its row)
-    const int blocks = colsum ? kPpoColBlocks : ((n + 3) / 4 < 2048 ? (n + 3) / 4 : 2048);
+    const int blocks = colsum ? kPpoColBlocks : ((n + 7) / 8 < 2048 ? (n + 7) / 8 : 2048);
     hipStream_t s = (hipStream_t)stream;
     const int esz = dtype == 0 ? 4 : 2;
     const int al = dtype == 0 ? 16 : 8;
@@ -243,4 +309,16 @@ extern "C" int bgx_ppo_head(const void* logits, int32_t dtype, int64_t ld_logits
     return bgx_ppo_head_ex(logits, dtype, ld_logits, values, records, actions, old_logp, returns, adv, n, n_actions,
                            eps_clip, c_value, c_entropy, grad_scale, dlogits, ld_dlogits, dvalues, sums, 0, nullptr,
                            stream);
+}
+
+extern "C" int bgx_relu_backward(void* dh, const void* h, int32_t n, int32_t hidden, float* colsum, int32_t blocks,
+                                 void* stream) {
+    if (n < 0 || hidden <= 0 || hidden % 8 || hidden > 256 || blocks <= 0 || !colsum ||
+        (n > 0 && (!dh || !h)))
+        return BGX_EINVAL;
+    if (((uintptr_t)dh | (uintptr_t)h) % 16) return BGX_EINVAL;
+    hipLaunchKernelGGL(k_relu_bwd, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (_Float16*)dh,
+                       (const _Float16*)h, n, hidden, colsum);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }

@@ -105,7 +105,7 @@ def test_update_matches_reference(golden, variant):
     moves by up to 4e-3 (lr 1e-3, first steps ~ lr * sign(g)), and fp16 rounding
     differences between CPU and GPU GEMMs flip the sign of a few near-zero
     gradient entries, which moves those weights by ~2e-3."""
-    from bgx.engine import encode
+    from bgx.engine import encode, encode_records
     from bgx.train import PPOTrainer
     g = golden("ppo_" + variant)
     N, T = int(g["N"]), int(g["T"])
@@ -114,6 +114,8 @@ def test_update_matches_reference(golden, variant):
     tr.net.load_state_dict(sd)
     rec = _records_from_fixture(g).cuda()
     assert torch.equal(encode(rec[:, :52].contiguous(), rec[:, 52].contiguous()).cpu(), torch.from_numpy(g["obs"]))
+    assert torch.equal(encode_records(rec).cpu(), torch.from_numpy(g["obs"]))
+    assert torch.equal(encode_records(rec, torch.float16).cpu(), torch.from_numpy(g["obs"]).half())
     tr.load_rollout(rec, torch.from_numpy(g["actions"]), torch.from_numpy(g["old_logp"]),
                     torch.from_numpy(g["old_v"]), torch.from_numpy(g["rewards"]), torch.from_numpy(g["dones"]))
     m = tr.update()
