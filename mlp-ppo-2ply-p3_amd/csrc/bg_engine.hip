@@ -298,47 +298,64 @@ __global__ __launch_bounds__(64) void k_encode(const int8_t* boards, const uint8
     }
 }
 
-// Feature f of the 64-byte record `rec` (board bytes 0..51, player to move at 52),
-// as feature_at (immutable_board.py:171-212).
-__device__ __forceinline__ float rec_feature(const uint8_t* rec, int f) {
-    if (f >= 196) return (f == 196) == (rec[R_CUR] == 0) ? 1.0f : 0.0f;
-    const int p = f >= 98 ? 1 : 0;
-    const int g = f - 98 * p;
-    if (g < 96) {
-        const int n = rec[p * 24 + (g >> 2)], u = g & 3;
-        if (u < 3) return n >= u + 1 ? 1.0f : 0.0f;
-        return n >= 3 ? (float)(n - 3) * 0.5f : 0.0f;
-    }
-    if (g == 96) return (float)rec[48 + p] * 0.5f;
-    return kOff15[rec[50 + p] & 15];
-}
-
 // The 198 features of n 64-byte lane records (the rollout's stored records), as
 // T = float or _Float16 (fp16: the rounding of the fp32 features that autocast's
-// cast applies, ppo_agent.py:274).  A 256-thread block stages 64 records in LDS
-// (one 16-byte load per thread) and writes their 64 x 198 outputs as contiguous
-// feature pairs (coalesced stores).
+// cast applies, ppo_agent.py:274), feature_at's encoding (immutable_board.py:171-212).
+// A 256-thread block encodes 64 consecutive records into an LDS image of their
+// contiguous output (64 x 198 T): one wave per record, lane l < 48 holding byte
+// l = the count of point l % 24 of player l / 24 (its 4 units at 98 (l / 24) +
+// 4 (l % 24)), lanes 48 / 49 (bar, off) of P1 / P2, lane 50 the one-hot; then the
+// block copies the image out with 16-byte stores (coalesced, whole lines).
+template <typename T>
+__device__ __forceinline__ void lds_pair(T* o, float a, float b) {
+    if (sizeof(T) == 2) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        h2 v; v[0] = (_Float16)a; v[1] = (_Float16)b;
+        *(h2*)o = v;
+    } else {
+        *(float2*)o = make_float2(a, b);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_encode_rec(const uint8_t* __restrict__ records, int n, T* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint8_t rec[64 * 64];
-    for (int r0 = blockIdx.x * 64; r0 < n; r0 += gridDim.x * 64) {
-        const int nr = min(64, n - r0);
-        __syncthreads();
-        if ((int)threadIdx.x < nr * 4)
-            ((uint4*)rec)[threadIdx.x] = ((const uint4*)(records + (size_t)r0 * 64))[threadIdx.x];
-        __syncthreads();
-        for (int q = threadIdx.x; q < nr * 99; q += blockDim.x) {
-            const int row = q / 99, f = 2 * (q - row * 99);
-            const uint8_t* rr = rec + row * 64;
-            const float a = rec_feature(rr, f), b = rec_feature(rr, f + 1);
-            T* o = out + (size_t)(r0 + row) * 198 + f;
-            if (sizeof(T) == 2) {
-                typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-                h2 v; v[0] = (_Float16)a; v[1] = (_Float16)b;
-                *(h2*)o = v;
-            } else {
-                *(float2*)o = make_float2(a, b);
+    constexpr int kRows = 64, kImg = kRows * 198 * (int)sizeof(T);        // bytes
+    __shared__ __attribute__((aligned(16))) uint8_t img[kImg];
+    T* im = (T*)img;
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int l2 = l == 48 ? 50 : (l == 49 ? 51 : 52);      // off1 / off2 / mover byte
+    for (int r0 = blockIdx.x * kRows; r0 < n; r0 += gridDim.x * kRows) {
+        const int nr = min(kRows, n - r0);
+        int b[16], b2[16];
+        #pragma unroll
+        for (int k = 0; k < 16; ++k) {                      // this wave's 16 records, loads in flight
+            const int r = r0 + w + 4 * k;
+            b[k] = r < n ? records[(size_t)r * 64 + l] : 0;
+            b2[k] = r < n ? records[(size_t)r * 64 + l2] : 0;
+        }
+        __syncthreads();                                    // the previous image is copied out
+        #pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            T* o = im + (w + 4 * k) * 198;
+            const int v = b[k], v2 = b2[k];
+            if (l < 48) {
+                const int P = l >= 24 ? 1 : 0, f = 98 * P + 4 * (l - 24 * P);
+                lds_pair(o + f, v >= 1 ? 1.0f : 0.0f, v >= 2 ? 1.0f : 0.0f);
+                lds_pair(o + f + 2, v >= 3 ? 1.0f : 0.0f, v >= 3 ? (float)(v - 3) * 0.5f : 0.0f);
+            } else if (l < 50) {
+                lds_pair(o + (l == 48 ? 96 : 194), (float)v * 0.5f, kOff15[v2 & 15]);
+            } else if (l == 50) {
+                lds_pair(o + 196, v2 == 0 ? 1.0f : 0.0f, v2 == 0 ? 0.0f : 1.0f);
             }
+        }
+        __syncthreads();
+        const int nbytes = nr * 198 * (int)sizeof(T);
+        uint8_t* dst = (uint8_t*)(out + (size_t)r0 * 198);
+        if (((uintptr_t)dst & 15) == 0) {
+            for (int q = threadIdx.x; q < nbytes / 16; q += blockDim.x) ((uint4*)dst)[q] = ((const uint4*)img)[q];
+            for (int q = (nbytes & ~15) + threadIdx.x; q < nbytes; q += blockDim.x) dst[q] = img[q];
+        } else {                                            // rows not 16-byte aligned: 4-byte copies
+            for (int q = threadIdx.x; q < nbytes / 4; q += blockDim.x) ((uint32_t*)dst)[q] = ((const uint32_t*)img)[q];
         }
     }
 }
@@ -766,7 +783,7 @@ int bgx_encode(const int8_t* boards52_dev, const uint8_t* players_dev, int32_t n
 int bgx_encode_records(const uint8_t* records_dev, int32_t n, int32_t dtype, void* out_dev, void* stream) {
     if (n < 0 || (dtype != 0 && dtype != 1) || (n > 0 && (!records_dev || !out_dev))) return BGX_EINVAL;
     if (n == 0) return BGX_OK;
-    const int blocks = (n + 63) / 64 < 8192 ? (n + 63) / 64 : 8192;
+    const int blocks = (n + 63) / 64 < 4096 ? (n + 63) / 64 : 4096;
     if (dtype == 0)
         hipLaunchKernelGGL(k_encode_rec<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, records_dev, n,
                            (float*)out_dev);

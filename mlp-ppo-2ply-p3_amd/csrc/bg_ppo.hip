@@ -23,6 +23,7 @@ constexpr int kPpoColBlocks = BGX_PPO_COLSUM_BLOCKS;
 // fp32 log(eps) and log(1 - eps), eps = FLT_EPSILON (torch clamp_probs bounds)
 constexpr float kLogEps = -15.942384719848633f;
 constexpr float kLog1mEps = -1.1920930376163597e-07f;
+constexpr float kL2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
 
 
 // Reductions over a 32-lane half-wave: DPP row_ror 8/4/2/1 inside each 16-lane row,
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
     const int j0 = C * c32;                                 // this lane's columns j0 .. j0+15
     const bool vload = vec && j0 + C <= ld_logits;
     const bool vstore = vec && j0 + C <= ld_dlogits && (pad || j0 + C <= A);
-    float s_pol = 0.0f, s_val = 0.0f, s_ent = 0.0f;      // per-half partials (<= a few hundred rows)
+    float s_pol = 0.0f, s_val = 0.0f, s_ent = 0.0f, s_gv = 0.0f;   // per-half partials (<= a few hundred rows)
     float cs[C];
     #pragma unroll
     for (int i = 0; i < C; ++i) cs[i] = 0.0f;
@@ -116,6 +117,8 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
         const float a = adv[row], olp = old_logp[row], ret = returns[row];
         const float v = (float)values[row];
         const float za = (float)lg[act] + (act < cnt ? 0.0f : kMaskLog);
+        // base-2 domain: z2 = (z + mask) log2(e) for the legal / masked columns,
+        // -inf past A (those columns do not exist in the reference's softmax)
         float z[C];
         if (vload) {
             Vec16<T>::load(lg + j0, z);
@@ -127,35 +130,35 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
         #pragma unroll
         for (int i = 0; i < C; ++i) {
             const int j = j0 + i;
-            z[i] = j < A ? z[i] + (j < cnt ? 0.0f : kMaskLog) : -INFINITY;
+            const float t = fmaf(z[i], kL2e, j < cnt ? 0.0f : kMaskLog * kL2e);
+            z[i] = j < A ? t : -INFINITY;
             m = fmaxf(m, z[i]);
         }
         BGX_HALF_REDUCE(fmaxf, m);
         float se = 0.0f;
         #pragma unroll
-        for (int i = 0; i < C; ++i) se += __expf(z[i] - m);          // exp(-inf) = 0
+        for (int i = 0; i < C; ++i) se += __builtin_amdgcn_exp2f(z[i] - m);     // exp2(-inf) = 0
         BGX_HALF_REDUCE(fadd, se);
-        const float lse = m + __logf(se);
+        const float lse2 = m + __log2f(se), nlse = -lse2 * kLn2;
         // torch.distributions.Categorical(probs) semantics (ppo_agent.py:273-291):
         // log_prob and entropy use L = log(clamp(p, eps, 1 - eps)) (clamp_probs),
         // whose gradient is zero outside [eps, 1 - eps].  z[i] <- p, q[i] <- L + in
-        float q[C], ent = 0.0f, s_in = 0.0f;
+        float q[C], ent = 0.0f, entq = 0.0f;
         #pragma unroll
         for (int i = 0; i < C; ++i) {
-            const float u = z[i] - lse;
-            const float inb = (u >= kLogEps && u <= kLog1mEps) ? 1.0f : 0.0f;
+            const float u = fmaf(z[i], kLn2, nlse);            // natural log-prob
             const float lp = fminf(fmaxf(u, kLogEps), kLog1mEps);
-            const float pi = __expf(u);
+            const float pi = __builtin_amdgcn_exp2f(z[i] - lse2);
             z[i] = pi;
-            q[i] = lp + inb;
-            ent -= pi * lp;                        // p = 0 off the legal set (and past A)
-            s_in += pi * inb;
+            q[i] = lp + (lp == u ? 1.0f : 0.0f);
+            ent = fmaf(-pi, lp, ent);                           // p = 0 past A
+            entq = fmaf(-pi, q[i], entq);
         }
         BGX_HALF_REDUCE(fadd, ent);
-        BGX_HALF_REDUCE(fadd, s_in);
-        const float ua = za - lse;
+        BGX_HALF_REDUCE(fadd, entq);
+        const float ua = za - lse2 * kLn2;
         const float la = fminf(fmaxf(ua, kLogEps), kLog1mEps);          // log pi(act), clamped
-        const float ina = (ua >= kLogEps && ua <= kLog1mEps) ? 1.0f : 0.0f;
+        const float ina = la == ua ? 1.0f : 0.0f;
         const float r = __expf(la - olp);
         const float s1 = r * a;
         const float rc = fminf(fmaxf(r, 1.0f - eps_clip), 1.0f + eps_clip);
@@ -167,34 +170,42 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
         const float g_lp = -a * r * (w1 + w2) * ina;
         // d/dz_k of  -min(.) - c_e * H  with H = -sum L_j p_j:
         //   g_lp (d_ka - p_k) + c_e p_k (L_k + in_k + H - sum_j p_j in_j)
-        const float ent_c = ent - s_in;
+        //   = p_k (K1 q_k + K2) + [k == a] gscale g_lp,  K1 = gscale c_e,
+        //   K2 = K1 (H - sum p in) - gscale g_lp,  H - sum p in = -sum p q
+        const float k1 = gscale * c_entropy, gla = gscale * g_lp, k2 = fmaf(k1, entq, -gla);
         const float dv = v - ret;
         const float gv = gscale * c_value * 2.0f * dv;
-        float g[C];
-        #pragma unroll
-        for (int i = 0; i < C; ++i) {
-            const float pi = z[i];
-            const int j = j0 + i;
-            const float gj = gscale * (g_lp * ((j == act ? 1.0f : 0.0f) - pi) + c_entropy * pi * (q[i] + ent_c));
-            // with `pad`: column A = the value gradient and zeros up to ld_dlogits
-            // (the layout of a [logits | value | 0] GEMM)
-            g[i] = j < A ? gj : (j == A ? gv : 0.0f);
-        }
+        // past A, p = 0 and g = 0: with `pad` the stored layout [logits | value | 0]
+        // gets the value gradient in column A (lane 0, after the row's vector stores)
         T* dl = dlogits + (int64_t)row * ld_dlogits;
         if (vstore) {
-            Vec16<T>::store(dl + j0, g);
             #pragma unroll
-            for (int i = 0; i < C; ++i) cs[i] += (float)(T)g[i];
+            for (int k = 0; k < C / 4; ++k) {
+                typedef T t4 __attribute__((ext_vector_type(4)));
+                t4 w;
+                #pragma unroll
+                for (int i = 4 * k; i < 4 * k + 4; ++i) {
+                    const T t = (T)fmaf(z[i], fmaf(k1, q[i], k2), j0 + i == act ? gla : 0.0f);
+                    w[i - 4 * k] = t;
+                    cs[i] += (float)t;
+                }
+                ((t4*)(dl + j0))[k] = w;
+            }
         } else {
             #pragma unroll
             for (int i = 0; i < C; ++i) {
                 const int j = j0 + i;
-                if (j < A || (pad && j < ld_dlogits)) {
-                    const T t = (T)g[i];
+                if (j < A || (pad && j < ld_dlogits && j != A)) {
+                    const T t = (T)fmaf(z[i], fmaf(k1, q[i], k2), j == act ? gla : 0.0f);
                     dl[j] = t;
                     cs[i] += (float)t;
                 }
             }
+        }
+        if (pad && c32 == 0) {
+            const T t = (T)gv;
+            dl[A] = t;
+            s_gv += (float)t;
         }
         if (c32 == 0) {
             dvalues[row] = (T)gv;
@@ -218,6 +229,8 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
         __shared__ float cred[8][512];
         #pragma unroll
         for (int i = 0; i < C; ++i) cred[half][j0 + i] = cs[i];
+        __syncthreads();
+        if (pad && c32 == 0) cred[half][A] += s_gv;      // column A: the stored value gradients
         __syncthreads();
         for (int c = threadIdx.x; c < 512; c += blockDim.x) {
             float t = 0.0f;

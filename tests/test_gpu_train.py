@@ -17,6 +17,12 @@ def test_trainer_iteration():
     assert m["env_steps"] == 2048 * 12
     assert any(not torch.equal(a, b) for a, b in zip(w0, tr.net.parameters()))
     recs = tr.buf["records"]
+    # the update's record encoder == the board encoder (G2-pinned) on every rollout row
+    from bgx.engine import encode, encode_records
+    flat = recs.reshape(-1, 64)
+    f32 = encode(flat[:, :52].contiguous(), flat[:, 52].contiguous())
+    assert torch.equal(encode_records(flat), f32)
+    assert torch.equal(encode_records(flat, torch.float16), f32.half())
     counts = (recs[..., 60].int() | (recs[..., 61].int() << 8))
     acts = tr.buf["actions"]
     assert bool(((acts < counts) | (counts == 0)).all())
