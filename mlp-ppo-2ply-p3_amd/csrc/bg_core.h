@@ -115,6 +115,24 @@ __device__ __forceinline__ Sub child(const Node& s, const Kids& k, int b, int d,
     return m;
 }
 
+// Canonical sub-move order (exact pruning of commuted duplicates, DESIGN.md
+// §3.1).  Two consecutive NORMAL sub-moves A (source a, child bit a) then B
+// (source b < a) with b != dst(A) commute: from the node before A, B is a child
+// (its checker, its unblocked destination and the node state do not depend on
+// A), A is a child after B, and both orders give the same node (same counts,
+// same hit set).  The order (B, A) comes first in the DFS (bit b < bit a), so
+// every leaf below (A, B) repeats one below (B, A): the walk skips it.  The
+// smallest-key path to any state is never skipped (its prefixes are smallest-key
+// too), so the visited set keeps every first occurrence, in DFS order, and the
+// memo's revisit argument is unchanged.  Children allowed after a sub-move with
+// child bit `bit` (31 = bar entry / bear-off: no restriction) and die d: bits
+// >= bit, plus, for PLAYER2 (moving down), the chain bit bit - d.
+__device__ __forceinline__ uint32_t canon_mask(int bit, int d, int pl) {
+    if (bit >= 24) return 0xFFFFFFFFu;
+    const uint32_t ge = ~((1u << bit) - 1u);
+    return pl == 0 ? ge : ge | (bit >= d ? 1u << (bit - d) : 0u);
+}
+
 // move_checker (immutable_board.py:42-89) on the bitboard state; generated
 // sub-moves never take the reference's "invalid" branches.
 __device__ __forceinline__ Node apply(const Node& s, const Sub& m, int pl) {
@@ -509,7 +527,11 @@ struct Gen {
 
     // handle_non_doubles (handle_moves.py:109-200); the pre-scan (:144-155) is
     // one ballot over the lane-parallel first level.
-    __device__ __forceinline__ void pass_nd(const Node& s0, int da, int db) {
+    // Second pass (lo then hi): a two-step (B, A) of two NORMAL sub-moves whose A
+    // does not move B's checker on (a != dst(B)) commutes (the argument of
+    // canon_mask with the dice swapped): (A, B) is a two-step of the first pass,
+    // already inserted, so only chain moves and bar entries / bear-offs remain.
+    __device__ __forceinline__ void pass_nd(const Node& s0, int da, int db, bool second) {
         const Kids k1 = gen(s0, da, pl, blocked);
         Node t1;
         uint32_t e1 = 0;
@@ -521,6 +543,8 @@ struct Gen {
             batch(a1, t1, (uint64_t)e1, 1);
             return;
         }
+        const int l = threadIdx.x & 63;
+        if (second && a1 && l < 24) q2 &= (1u << 31) | (1u << (pl == 0 ? l + da : l - da));
         flat_leaves(__ballot(a1 && q2 != 0u), t1, q2, x2, (uint64_t)e1, db, 16, 2);
     }
 
@@ -586,15 +610,17 @@ struct Gen {
                                 ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(penc2 >> 32), src) << 32);
             Node t3;
             uint64_t pe3 = 0;
+            int cb = 31;
             if (valid) {
-                const Sub m = child(s2, k, select_bit(qb, j), d, pl);
+                cb = select_bit(qb, j);
+                const Sub m = child(s2, k, cb, d, pl);
                 t3 = apply(s2, m, pl);
                 pe3 = Sink::kEnc ? pe | ((uint64_t)m.enc << 32) : 0ull;
             }
             const uint64_t f3 = memo_batch<kLogMemo3, true>(memo3, n_memo3, valid, t3, kTag3);
             uint32_t q4 = 0;
             int x4 = -1;
-            if ((f3 >> l) & 1ull) { const Kids kk = gen(t3, d, pl, blocked); q4 = kk.bits; x4 = kk.extra; }
+            if ((f3 >> l) & 1ull) { const Kids kk = gen(t3, d, pl, blocked); q4 = kk.bits & canon_mask(cb, d, pl); x4 = kk.extra; }
             flat_leaves(__ballot(((f3 >> l) & 1ull) && q4 != 0u), t3, q4, x4, pe3, d, 48, 4);
             if (ovf) return;
         }
@@ -627,15 +653,17 @@ struct Gen {
             const uint64_t pe = !Sink::kEnc ? 0ull : (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc1, src);
             Node t2;
             uint64_t pe2 = 0;
+            int cb = 31;
             if (valid) {
-                const Sub m = child(s1, k, select_bit(qb, j), d, pl);
+                cb = select_bit(qb, j);
+                const Sub m = child(s1, k, cb, d, pl);
                 t2 = apply(s1, m, pl);
                 pe2 = Sink::kEnc ? pe | ((uint64_t)m.enc << 16) : 0ull;
             }
             const uint64_t f2 = memo_batch<kLogMemo2, true>(memo2, n_memo2, valid, t2, kTag2);
             uint32_t q3 = 0;
             int x3 = -1;
-            if ((f2 >> l) & 1ull) { const Kids kk = gen(t2, d, pl, blocked); q3 = kk.bits; x3 = kk.extra; }
+            if ((f2 >> l) & 1ull) { const Kids kk = gen(t2, d, pl, blocked); q3 = kk.bits & canon_mask(cb, d, pl); x3 = kk.extra; }
             flat_depth3(__ballot(((f2 >> l) & 1ull) && q3 != 0u), t2, q3, x3, pe2, d);
             if (ovf) return;
         }
@@ -654,23 +682,26 @@ struct Gen {
         bool got4 = false;
         BG_CNT(0, 1);
         BG_T0(t_phase_a);
+        const int l = threadIdx.x & 63;
+        // q*: a node's child list (dead-end test); c*: the children the walk
+        // visits (canon_mask of the node's own child bit, which is its lane here)
         const Kids k1 = gen(s0, d, pl, blocked);
         Node t1;
         uint32_t e1 = 0;
         const bool a1 = lane_child(s0, k1, d, t1, e1);
-        uint32_t q2 = 0;
+        uint32_t q2 = 0, c2 = 0;
         int x2 = -1;
-        if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; x2 = k.extra; }
+        if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; c2 = q2 & canon_mask(l, d, pl); x2 = k.extra; }
         for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
             if (got4) {
-                flat_depth2((uint64_t)b1 & __ballot(q2 != 0u), t1, q2, x2, (uint64_t)e1, d);
+                flat_depth2((uint64_t)b1 & __ballot(c2 != 0u), t1, c2, x2, (uint64_t)e1, d);
                 return;
             }
             const int i1 = __builtin_ctz(b1);
             const Node s1 = rd_node(t1, i1);
-            const Kids k2{rdl(q2, i1), (int)rdl((uint32_t)x2, i1)};
+            const Kids k2{rdl(c2, i1), (int)rdl((uint32_t)x2, i1)};
             const uint64_t m1 = rdl(e1, i1);
-            if (!k2.bits) {
+            if (!rdl(q2, i1)) {
                 if (!got4) { insert(s1, m1, 1); if (ovf) return; }
                 continue;
             }
@@ -679,20 +710,20 @@ struct Gen {
             const bool a2 = lane_child(s1, k2, d, t2, e2l);
             const uint64_t f2 = memo_batch<kLogMemo2>(memo2, n_memo2, a2, t2, kTag2);
             BG_CNT(3, __popcll(f2));
-            uint32_t q3 = 0;
+            uint32_t q3 = 0, c3 = 0;
             int x3 = -1;
-            if ((f2 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; x3 = k.extra; }
+            if ((f2 >> l) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; c3 = q3 & canon_mask(l, d, pl); x3 = k.extra; }
             for (uint64_t b2 = f2; b2; b2 &= b2 - 1ull) {
                 if (got4) {
-                    flat_depth3(b2 & __ballot(q3 != 0u), t2, q3, x3, m1 | ((uint64_t)e2l << 16), d);
+                    flat_depth3(b2 & __ballot(c3 != 0u), t2, c3, x3, m1 | ((uint64_t)e2l << 16), d);
                     if (ovf) return;
                     break;
                 }
                 const int i2 = __ffsll((unsigned long long)b2) - 1;
                 const Node s2 = rd_node(t2, i2);
-                const Kids k3{rdl(q3, i2), (int)rdl((uint32_t)x3, i2)};
+                const Kids k3{rdl(c3, i2), (int)rdl((uint32_t)x3, i2)};
                 const uint64_t m2 = m1 | ((uint64_t)rdl(e2l, i2) << 16);
-                if (!k3.bits) {
+                if (!rdl(q3, i2)) {
                     if (!got4) { insert(s2, m2, 2); if (ovf) return; }
                     continue;
                 }
@@ -701,13 +732,12 @@ struct Gen {
                 const bool a3 = lane_child(s2, k3, d, t3, e3l);
                 const uint64_t f3 = memo_batch<kLogMemo3>(memo3, n_memo3, a3, t3, kTag3);
                 BG_CNT(5, __popcll(f3));
-                uint32_t q4 = 0;
+                uint32_t q4 = 0, c4 = 0;
                 int x4 = -1;
-                if ((f3 >> (threadIdx.x & 63)) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; x4 = k.extra; }
+                if ((f3 >> l) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; c4 = q4 & canon_mask(l, d, pl); x4 = k.extra; }
                 for (uint64_t b3 = f3; b3; b3 &= b3 - 1ull) {
                     const int i3 = __ffsll((unsigned long long)b3) - 1;
-                    const uint32_t kb = rdl(q4, i3);
-                    if (!kb) {
+                    if (!rdl(q4, i3)) {
                         if (!got4) {
                             insert(rd_node(t3, i3), m2 | ((uint64_t)rdl(e3l, i3) << 32), 3);
                             if (ovf) return;
@@ -716,9 +746,11 @@ struct Gen {
                     }
                     // from the first node with children on, got4 holds: dead ends are
                     // no-ops and every remaining node's leaves go out as one flat batch
-                    const uint64_t rest = b3 & __ballot(q4 != 0u);
+                    // (that node's first visited child is the walk's first 4-long leaf:
+                    // a skipped one would repeat an earlier 4-long leaf)
+                    const uint64_t rest = b3 & __ballot(c4 != 0u);
                     BG_T1(9, t_phase_a); BG_CNT(10, 1);
-                    flat_leaves(rest, t3, q4, x4, m2 | ((uint64_t)e3l << 32), d, 48, 4);
+                    flat_leaves(rest, t3, c4, x4, m2 | ((uint64_t)e3l << 32), d, 48, 4);
                     if (ovf) return;
                     got4 = true;
                     break;
@@ -731,9 +763,9 @@ struct Gen {
     __device__ __forceinline__ void run_nd(const Node& s0, int r0, int r1) {
         cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
         const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
-        pass_nd(s0, hi, lo);
+        pass_nd(s0, hi, lo, false);
         if (ovf) return;
-        if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi);   // :41-53
+        if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi, true);   // :41-53
     }
 
     // doubles only (r0 == r1 == d)
@@ -747,9 +779,9 @@ struct Gen {
         cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
         if (r0 != r1) {
             const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
-            pass_nd(s0, hi, lo);
+            pass_nd(s0, hi, lo, false);
             if (ovf) return;
-            if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi);   // :41-53
+            if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi, true);   // :41-53
         } else {
             doubles(s0, r0);
         }
