@@ -483,8 +483,10 @@ struct Gen {
     // chunks: leaf p of the chunk belongs to the parent whose prefix range holds
     // it and is that parent's (p - prefix)-th child.  Entries are
     // penc | enc << shift of length len.  Cousins may coincide: DEDUP commit.
+    // d_up >= 0: the children of parents on lanes 32-63 use die d_up (both
+    // non-doubles passes in one batch, nd_both).
     __device__ __forceinline__ void flat_leaves(uint64_t parents, const Node& t, uint32_t q, int x, uint64_t penc,
-                                                int d, int shift, int len) {
+                                                int d, int shift, int len, int d_up = -1) {
         const int l = threadIdx.x & 63;
         const bool par = (parents >> l) & 1ull;
         const uint32_t cnt = par ? (uint32_t)__popc(q) : 0u;         // <= 25
@@ -513,7 +515,7 @@ struct Gen {
             uint32_t slot = 0;
             bool found = true;
             if (valid) {
-                const Sub m = child(s, k, select_bit(qb, j), d, pl);
+                const Sub m = child(s, k, select_bit(qb, j), d_up >= 0 && src >= 32 ? d_up : d, pl);
                 leaf = apply(s, m, pl);
                 enc = Sink::kEnc ? pe | ((uint64_t)m.enc << shift) : 0ull;
                 BG_T0(tp);
@@ -525,27 +527,51 @@ struct Gen {
         }
     }
 
-    // handle_non_doubles (handle_moves.py:109-200); the pre-scan (:144-155) is
-    // one ballot over the lane-parallel first level.
-    // Second pass (lo then hi): a two-step (B, A) of two NORMAL sub-moves whose A
-    // does not move B's checker on (a != dst(B)) commutes (the argument of
-    // canon_mask with the dice swapped): (A, B) is a two-step of the first pass,
-    // already inserted, so only chain moves and bar entries / bear-offs remain.
-    __device__ __forceinline__ void pass_nd(const Node& s0, int da, int db, bool second) {
-        const Kids k1 = gen(s0, da, pl, blocked);
+    // handle_non_doubles (handle_moves.py:109-200) for both dice orders of
+    // get_all_possible_moves (get_all_moves.py:33-53) at once: lanes 0-31 hold the
+    // first level of pass 1 (hi then lo; lane = child bit), lanes 32-63 that of
+    // pass 2 (lo then hi); each pass's pre-scan (:144-155) is one ballot.
+    // * Pass 1 has a two-step: its entries are two-steps (cur_max 2 from its first,
+    //   never duplicate, leaf), so the skip rule (:41-53) cannot fire.  Pass 2 then
+    //   adds either two-steps -- in the same flat batch, after pass 1's (lane order
+    //   = insertion order; the first occurrence wins) -- or only singles, which can
+    //   never survive the max-length filter: skipped.
+    // * Otherwise the passes run in order (pass 1's singles, the skip rule, pass 2).
+    // Pass 2's two-step (B, A) of two NORMAL sub-moves where A does not move B's
+    // checker on (a != dst(B)) commutes (the argument of canon_mask with the dice
+    // swapped): (A, B) is a pass-1 two-step, already inserted, so only chain moves
+    // and bar entries / bear-offs are walked.
+    __device__ __forceinline__ void nd_both(const Node& s0, int hi, int lo) {
+        const int l = threadIdx.x & 63;
+        const bool up = l >= 32;
+        const int bit = l & 31, da = up ? lo : hi, db = up ? hi : lo;
+        const Kids kh = gen(s0, hi, pl, blocked), kl = gen(s0, lo, pl, blocked);
+        const Kids k1{up ? kl.bits : kh.bits, up ? kl.extra : kh.extra};
+        const bool a1 = (k1.bits >> bit) & 1u;
         Node t1;
-        uint32_t e1 = 0;
-        const bool a1 = lane_child(s0, k1, da, t1, e1);
-        uint32_t q2 = 0;
+        uint32_t e1 = 0, q2 = 0;
         int x2 = -1;
-        if (a1) { const Kids k = gen(t1, db, pl, blocked); q2 = k.bits; x2 = k.extra; }
-        if (__ballot(a1 && q2 != 0u) == 0ull) {       // no two-dice sequence: the singles
-            batch(a1, t1, (uint64_t)e1, 1);
+        if (a1) {
+            const Sub m = child(s0, k1, bit, da, pl);
+            t1 = apply(s0, m, pl);
+            e1 = Sink::kEnc ? m.enc : 0u;
+            const Kids k = gen(t1, db, pl, blocked);
+            q2 = k.bits;
+            x2 = k.extra;
+        }
+        constexpr uint64_t kLow = 0xFFFFFFFFull;
+        const uint64_t two = __ballot(a1 && q2 != 0u);
+        if (two & kLow) {
+            if (up && a1 && bit < 24) q2 &= (1u << 31) | (1u << (pl == 0 ? bit + da : bit - da));
+            uint64_t par = __ballot(a1 && q2 != 0u);
+            if (!(two >> 32)) par &= kLow;
+            flat_leaves(par, t1, q2, x2, (uint64_t)e1, lo, 16, 2, hi);
             return;
         }
-        const int l = threadIdx.x & 63;
-        if (second && a1 && l < 24) q2 &= (1u << 31) | (1u << (pl == 0 ? l + da : l - da));
-        flat_leaves(__ballot(a1 && q2 != 0u), t1, q2, x2, (uint64_t)e1, db, 16, 2);
+        batch(a1 && !up, t1, (uint64_t)e1, 1);                  // pass 1: singles
+        if (ovf || (n_unique == 1 && cur_max == 1)) return;     // :41-53
+        if (two) flat_leaves(two, t1, q2, x2, (uint64_t)e1, hi, 16, 2);
+        else batch(a1 && up, t1, (uint64_t)e1, 1);
     }
 
     // Revisit check of a sibling batch at one depth: returns the lanes not seen
@@ -763,9 +789,7 @@ struct Gen {
     __device__ __forceinline__ void run_nd(const Node& s0, int r0, int r1) {
         cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
         const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
-        pass_nd(s0, hi, lo, false);
-        if (ovf) return;
-        if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi, true);   // :41-53
+        nd_both(s0, hi, lo);
     }
 
     // doubles only (r0 == r1 == d)
@@ -779,9 +803,7 @@ struct Gen {
         cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
         if (r0 != r1) {
             const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
-            pass_nd(s0, hi, lo, false);
-            if (ovf) return;
-            if (!(n_unique == 1 && cur_max == 1)) pass_nd(s0, lo, hi, true);   // :41-53
+            nd_both(s0, hi, lo);
         } else {
             doubles(s0, r0);
         }
