@@ -125,12 +125,26 @@ __device__ __forceinline__ Sub child(const Node& s, const Kids& k, int b, int d,
 // smallest-key path to any state is never skipped (its prefixes are smallest-key
 // too), so the visited set keeps every first occurrence, in DFS order, and the
 // memo's revisit argument is unchanged.  Children allowed after a sub-move with
-// child bit `bit` (31 = bar entry / bear-off: no restriction) and die d: bits
-// >= bit, plus, for PLAYER2 (moving down), the chain bit bit - d.
-__device__ __forceinline__ uint32_t canon_mask(int bit, int d, int pl) {
+// child bit `bit` (31 = bar entry / bear-off: no restriction) and die d, t = the
+// node after it: bits >= bit, plus, for PLAYER2 (moving down), the chain bit
+// bit - d when the moved checker is alone there (with another checker already
+// there, moving that one first is the same pair in the smaller order).
+// PLAYER1 walks that cannot bear off visit every state exactly once (a state's
+// sub-move multiset is recovered from its count changes, point by point from
+// the far end, and the ascending order of that multiset is its only visited
+// path), so they run without table or memo (Gen::pure_walk; tools/check_canon.py
+// checks it on random positions).
+// mirror (PLAYER2 walks that cannot bear off, set semantics only -- the 2-ply
+// replies): bits <= bit, the mirror image of PLAYER1's order, again one visit per
+// state; the set of afterstates is the same, their order is not.
+__device__ __forceinline__ uint32_t canon_mask(int bit, int d, int pl, const Node& t, bool mirror = false) {
     if (bit >= 24) return 0xFFFFFFFFu;
+    if (mirror) return (1u << 31) | ((2u << bit) - 1u);
     const uint32_t ge = ~((1u << bit) - 1u);
-    return pl == 0 ? ge : ge | (bit >= d ? 1u << (bit - d) : 0u);
+    if (pl == 0 || bit < d) return ge;
+    const int c = bit - d;
+    const uint64_t w = c < 16 ? t.lo : (uint64_t)t.hi;
+    return ((w >> (4 * (c & 15))) & 15u) == 1u ? ge | (1u << c) : ge;
 }
 
 // move_checker (immutable_board.py:42-89) on the bitboard state; generated
@@ -381,6 +395,7 @@ constexpr int kLogCMemo = 9;      // MEMO_KIND 1: depth-2 and depth-3 entries sh
 // (first `cap` entries).  Other sinks (bg_search.hip) keep afterstate keys.
 struct MoveSink {
     static constexpr bool kEnc = true;     // needs the move encodings
+    static constexpr bool kSet = false;    // the ORDERED list (first occurrences in DFS order)
     uint64_t* out;      // this game's move list, `cap` entries
     int cap;
     __device__ __forceinline__ void reset() {}
@@ -414,15 +429,19 @@ struct Gen {
     uint32_t blocked;
     int cur_max, count, n_unique, cap_unique;
     bool ovf;
+    bool pure_walk = false;   // this doubles walk visits every state once: no table, no memo
+    bool mirror = false;      // ... in PLAYER2's mirrored order (set semantics only)
 
     // table slots in use (dedup entries + tagged memo entries)
     __device__ __forceinline__ int fill() const { return n_unique + (TAGGED ? n_memo2 + n_memo3 : 0); }
 
     __device__ __forceinline__ void insert(const Node& s, uint64_t enc, int len) {
         const uint32_t a = (uint32_t)s.lo, b = (uint32_t)(s.lo >> 32);
-        if (!table_insert<LOG_SLOTS>(tab, a, b, s.hi, s.k3)) return;
-        ++n_unique;
-        if (fill() >= cap_unique) { ovf = true; return; }
+        if (!pure_walk) {
+            if (!table_insert<LOG_SLOTS>(tab, a, b, s.hi, s.k3)) return;
+            ++n_unique;
+            if (fill() >= cap_unique) { ovf = true; return; }
+        }
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
             sink.push(s, enc, count, len);
@@ -445,18 +464,25 @@ struct Gen {
 
     // Add the entries of the lanes in `fresh` (length len), in lane order.
     // DEDUP: the batch may hold equal keys (cousins); first one wins.
+    // pure: lanes whose entry is known to be new and never met again (nd_both's
+    // pure two-steps): listed without a table slot.
     template <bool DEDUP = false>
-    __device__ __forceinline__ void commit(uint64_t fresh, const Node& t, uint64_t enc, uint32_t slot, int len) {
+    __device__ __forceinline__ void commit(uint64_t fresh, const Node& t, uint64_t enc, uint32_t slot, int len,
+                                           uint64_t pure = 0ull) {
         int n = __popcll(fresh);
-        if (!n) return;
-        BG_T0(tc);
-        if (fill() + n >= cap_unique) { ovf = true; return; }
-        fresh = place_batch<LOG_SLOTS, DEDUP>(tab, fresh, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
-        BG_T1(13, tc);
-        BG_CNT(2, 1);
-        if (DEDUP) n = __popcll(fresh);
+        if (!n && !pure) return;
+        if (n) {
+            BG_T0(tc);
+            if (fill() + n >= cap_unique) { ovf = true; return; }
+            fresh = place_batch<LOG_SLOTS, DEDUP>(tab, fresh, (uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3, slot);
+            BG_T1(13, tc);
+            BG_CNT(2, 1);
+            if (DEDUP) n = __popcll(fresh);
+            n_unique += n;
+        }
+        fresh |= pure;
+        n = __popcll(fresh);
         BG_CNT(8, n);
-        n_unique += n;
         if (len > cur_max) { cur_max = len; count = 0; sink.reset(); }
         if (len == cur_max) {
             BG_T0(ts);
@@ -483,8 +509,16 @@ struct Gen {
     // chunks: leaf p of the chunk belongs to the parent whose prefix range holds
     // it and is that parent's (p - prefix)-th child.  Entries are
     // penc | enc << shift of length len.  Cousins may coincide: DEDUP commit.
-    // d_up >= 0: the children of parents on lanes 32-63 use die d_up (both
-    // non-doubles passes in one batch, nd_both).
+    // d_up >= 0: both non-doubles passes in one batch (nd_both): parents on lanes
+    // 0-31 are pass 1's first sub-moves (die d_up, child bit = lane), their
+    // children use die d; parents on lanes 32-63 are pass 2's, children die d_up.
+    // A pass-1 two-step (A, B) of two NORMAL sub-moves with b != dst(A) (no chain)
+    // and dst(B) != a (no reverse chain) is PURE: its count change is -1 at a and
+    // b, +1 at dst(A) and dst(B) with nothing cancelling, which only the same pair
+    // produces within pass 1; every other walked entry either has a cancelling
+    // pair (chains: one checker moved by both dice) or changes the bar / off
+    // counts (bar entries, bear-offs), and pass 2 walks no other kind
+    // (nd_both).  So a pure entry is new and is never met again: no table slot.
     __device__ __forceinline__ void flat_leaves(uint64_t parents, const Node& t, uint32_t q, int x, uint64_t penc,
                                                 int d, int shift, int len, int d_up = -1) {
         const int l = threadIdx.x & 63;
@@ -513,16 +547,23 @@ struct Gen {
             Node leaf;
             uint64_t enc = 0;
             uint32_t slot = 0;
-            bool found = true;
+            bool found = true, pure = false;
             if (valid) {
-                const Sub m = child(s, k, select_bit(qb, j), d_up >= 0 && src >= 32 ? d_up : d, pl);
+                const int cb = select_bit(qb, j);
+                const Sub m = child(s, k, cb, d_up >= 0 && src >= 32 ? d_up : d, pl);
                 leaf = apply(s, m, pl);
                 enc = Sink::kEnc ? pe | ((uint64_t)m.enc << shift) : 0ull;
+                if (d_up >= 0 && src < 24 && cb < 24) {
+                    const int dst_a = pl == 0 ? src + d_up : src - d_up;
+                    pure = cb != dst_a && m.dst != src;
+                }
+                pure = pure || pure_walk;
                 BG_T0(tp);
-                found = probe_lane<LOG_SLOTS>(tab, (uint32_t)leaf.lo, (uint32_t)(leaf.lo >> 32), leaf.hi, leaf.k3, slot);
+                if (!pure)
+                    found = probe_lane<LOG_SLOTS>(tab, (uint32_t)leaf.lo, (uint32_t)(leaf.lo >> 32), leaf.hi, leaf.k3, slot);
                 BG_T1(12, tp);
             }
-            commit<true>(__ballot(valid && !found), leaf, enc, slot, len);
+            commit<true>(__ballot(valid && !pure && !found), leaf, enc, slot, len, __ballot(valid && pure));
             if (ovf) return;
         }
     }
@@ -580,7 +621,7 @@ struct Gen {
     // the visit, later ones are revisits (pruned) -- when recorded.
     template <int LOGM, bool DEDUP = false>
     __device__ __forceinline__ uint64_t memo_batch(uint4* memo, int& nm, bool act, const Node& t, uint32_t tag) {
-        if (!memo) return __ballot(act);
+        if (!memo || pure_walk) return __ballot(act);
         constexpr int LOGT = MEMO_KIND == 1 ? kLogCMemo : LOGM;
         uint32_t slot = 0;
         bool found = true;
@@ -646,7 +687,7 @@ struct Gen {
             const uint64_t f3 = memo_batch<kLogMemo3, true>(memo3, n_memo3, valid, t3, kTag3);
             uint32_t q4 = 0;
             int x4 = -1;
-            if ((f3 >> l) & 1ull) { const Kids kk = gen(t3, d, pl, blocked); q4 = kk.bits & canon_mask(cb, d, pl); x4 = kk.extra; }
+            if ((f3 >> l) & 1ull) { const Kids kk = gen(t3, d, pl, blocked); q4 = kk.bits & canon_mask(cb, d, pl, t3, mirror); x4 = kk.extra; }
             flat_leaves(__ballot(((f3 >> l) & 1ull) && q4 != 0u), t3, q4, x4, pe3, d, 48, 4);
             if (ovf) return;
         }
@@ -689,7 +730,7 @@ struct Gen {
             const uint64_t f2 = memo_batch<kLogMemo2, true>(memo2, n_memo2, valid, t2, kTag2);
             uint32_t q3 = 0;
             int x3 = -1;
-            if ((f2 >> l) & 1ull) { const Kids kk = gen(t2, d, pl, blocked); q3 = kk.bits & canon_mask(cb, d, pl); x3 = kk.extra; }
+            if ((f2 >> l) & 1ull) { const Kids kk = gen(t2, d, pl, blocked); q3 = kk.bits & canon_mask(cb, d, pl, t2, mirror); x3 = kk.extra; }
             flat_depth3(__ballot(((f2 >> l) & 1ull) && q3 != 0u), t2, q3, x3, pe2, d);
             if (ovf) return;
         }
@@ -709,6 +750,10 @@ struct Gen {
         BG_CNT(0, 1);
         BG_T0(t_phase_a);
         const int l = threadIdx.x & 63;
+        // no bear-off within 4 sub-moves: more than 3 checkers off the home board
+        // (bar included; 15 - home - off, which only over-counts a short board)
+        pure_walk = 15 - s0.n_home - (int)((s0.k3 >> 4) & 15u) > 3 && (pl == 0 || Sink::kSet);
+        mirror = pure_walk && pl == 1;
         // q*: a node's child list (dead-end test); c*: the children the walk
         // visits (canon_mask of the node's own child bit, which is its lane here)
         const Kids k1 = gen(s0, d, pl, blocked);
@@ -717,7 +762,7 @@ struct Gen {
         const bool a1 = lane_child(s0, k1, d, t1, e1);
         uint32_t q2 = 0, c2 = 0;
         int x2 = -1;
-        if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; c2 = q2 & canon_mask(l, d, pl); x2 = k.extra; }
+        if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; c2 = q2 & canon_mask(l, d, pl, t1, mirror); x2 = k.extra; }
         for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
             if (got4) {
                 flat_depth2((uint64_t)b1 & __ballot(c2 != 0u), t1, c2, x2, (uint64_t)e1, d);
@@ -738,7 +783,7 @@ struct Gen {
             BG_CNT(3, __popcll(f2));
             uint32_t q3 = 0, c3 = 0;
             int x3 = -1;
-            if ((f2 >> l) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; c3 = q3 & canon_mask(l, d, pl); x3 = k.extra; }
+            if ((f2 >> l) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; c3 = q3 & canon_mask(l, d, pl, t2, mirror); x3 = k.extra; }
             for (uint64_t b2 = f2; b2; b2 &= b2 - 1ull) {
                 if (got4) {
                     flat_depth3(b2 & __ballot(c3 != 0u), t2, c3, x3, m1 | ((uint64_t)e2l << 16), d);
@@ -760,7 +805,7 @@ struct Gen {
                 BG_CNT(5, __popcll(f3));
                 uint32_t q4 = 0, c4 = 0;
                 int x4 = -1;
-                if ((f3 >> l) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; c4 = q4 & canon_mask(l, d, pl); x4 = k.extra; }
+                if ((f3 >> l) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; c4 = q4 & canon_mask(l, d, pl, t3, mirror); x4 = k.extra; }
                 for (uint64_t b3 = f3; b3; b3 &= b3 - 1ull) {
                     const int i3 = __ffsll((unsigned long long)b3) - 1;
                     if (!rdl(q4, i3)) {
@@ -787,20 +832,20 @@ struct Gen {
 
     // non-doubles only (r0 != r1): the same as run() without the doubles code
     __device__ __forceinline__ void run_nd(const Node& s0, int r0, int r1) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false;
         const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
         nd_both(s0, hi, lo);
     }
 
     // doubles only (r0 == r1 == d)
     __device__ __forceinline__ void run_d(const Node& s0, int d) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false;
         doubles(s0, d);
     }
 
     // get_all_possible_moves (get_all_moves.py:9-70)
     __device__ __forceinline__ void run(const Node& s0, int r0, int r1) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false;
         if (r0 != r1) {
             const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
             nd_both(s0, hi, lo);

@@ -148,6 +148,7 @@ __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
 // (re-run next round); its leaves already written stay valid candidates.
 struct KeySink {
     static constexpr bool kEnc = false;    // keys only: the move encodings are dead
+    static constexpr bool kSet = true;     // the SET of afterstates (min over replies): order is free
     uint4* keys;
     uint32_t* tags;
     unsigned long long* cursor;
