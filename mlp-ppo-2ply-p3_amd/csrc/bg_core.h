@@ -190,13 +190,15 @@ __device__ __forceinline__ bool key_empty(const uint4& v) { return opaque(v.x | 
 // Open addressing, linear probing, empty == all-zero key (a real afterstate
 // always has a non-zero own count/bar/off).  The whole wave probes 64
 // consecutive slots per step.  Never more than 7/8 full (callers enforce).
+// Every probe loop is bounded by the table size (a hang guard: a valid table
+// always stops them long before).
 template <int LOG_SLOTS, typename SlotPtr>
 __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d,
                                              bool may_insert = true) {
     constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
     const int lane = threadIdx.x & 63;
     uint32_t base = key_hash(a, b, c, d);
-    for (;;) {
+    for (uint32_t it = 0; it <= (mask >> 6) + 1u; ++it) {
         const uint32_t slot = (base + (uint32_t)lane) & mask;
         const uint4 v = tab[slot];
         const bool eq = key_eq(v, a, b, c, d);
@@ -211,6 +213,7 @@ __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b
         }
         base += 64u;
     }
+    return false;
 }
 
 // Per-lane (divergent) membership test along the same linear probe sequence.
@@ -218,12 +221,13 @@ template <int LOG_SLOTS, typename SlotPtr>
 __device__ __forceinline__ bool table_contains_lane(SlotPtr tab, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
     uint32_t h = key_hash(a, b, c, d) & mask;
-    for (;;) {
+    for (uint32_t it = 0; it <= mask; ++it) {
         const uint4 v = tab[h];
         if (key_eq(v, a, b, c, d)) return true;
         if (key_empty(v)) return false;
         h = (h + 1u) & mask;
     }
+    return false;
 }
 
 __device__ __forceinline__ uint32_t rdl(uint32_t v, int lane) {
@@ -239,7 +243,7 @@ __device__ __forceinline__ bool probe_lane(SlotPtr tab, uint32_t a, uint32_t b, 
                                            uint32_t& slot) {
     constexpr uint32_t mask = (1u << LOG_SLOTS) - 1u;
     uint32_t h = key_hash(a, b, c, d) & mask;
-    for (;;) {
+    for (uint32_t it = 0; it <= (mask >> 2); ++it) {
         uint4 v0 = tab[h], v1 = tab[(h + 1u) & mask], v2 = tab[(h + 2u) & mask], v3 = tab[(h + 3u) & mask];
         // all four reads in flight before the first use (one wait, not four)
         __asm__ volatile("" : "+v"(v0.x), "+v"(v1.x), "+v"(v2.x), "+v"(v3.x));
@@ -255,6 +259,8 @@ __device__ __forceinline__ bool probe_lane(SlotPtr tab, uint32_t a, uint32_t b, 
         }
         h = (h + 4u) & mask;
     }
+    slot = h;
+    return true;
 }
 
 // Insert the keys of the lanes in `fresh`, each lane's `slot` from probe_lane
@@ -299,10 +305,11 @@ __device__ __forceinline__ uint64_t place_batch(SlotPtr tab, uint64_t fresh, uin
         if (!pend) break;
         bool drop = false;
         if ((pend >> lane) & 1ull) {
-            for (;;) {
+            drop = true;
+            for (uint32_t it = 0; it <= mask; ++it) {
                 const uint4 v = tab[slot];
-                if (DEDUP && key_eq(v, a, b, c, d)) { drop = true; break; }
-                if (key_empty(v)) break;
+                if (DEDUP && key_eq(v, a, b, c, d)) break;
+                if (key_empty(v)) { drop = false; break; }
                 slot = (slot + 1u) & mask;
             }
         }
@@ -431,6 +438,23 @@ struct Gen {
     bool ovf;
     bool pure_walk = false;   // this doubles walk visits every state once: no table, no memo
     bool mirror = false;      // ... in PLAYER2's mirrored order (set semantics only)
+    bool nd_free = false;     // nd_both's two-steps decided without the table (flat_leaves)
+    bool clean = false;       // table (and memo) cleared for this run: callers leave it
+                              // dirty and the walk clears it only if it needs it
+    uint32_t root_occ = 0, root_blot = 0;
+
+    // clear the dedup table and the separate memo tables before first use
+    __device__ __forceinline__ void need_table() {
+        if (clean) return;
+        const int l = threadIdx.x & 63;
+        for (int i = l; i < (1 << LOG_SLOTS); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (MEMO_KIND != 2 && memo2) {
+            constexpr int n = MEMO_KIND == 1 ? (1 << kLogCMemo) : kMemoSlots;
+            for (int i = l; i < n; i += 64) memo2[i] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        clean = true;
+    }
 
     // table slots in use (dedup entries + tagged memo entries)
     __device__ __forceinline__ int fill() const { return n_unique + (TAGGED ? n_memo2 + n_memo3 : 0); }
@@ -556,13 +580,17 @@ struct Gen {
                 if (d_up >= 0 && src < 24 && cb < 24) {
                     const int dst_a = pl == 0 ? src + d_up : src - d_up;
                     pure = cb != dst_a && m.dst != src;
+                    if (nd_free && !pure) pure = nd_first(cb == dst_a ? src : cb, cb == dst_a ? 1 : 2, d, d_up);
+                } else if (nd_free) {
+                    pure = nd_first(src - 32, 3, d, d_up);      // pass 2: a chain (no specials here)
                 }
                 pure = pure || pure_walk;
                 BG_T0(tp);
-                if (!pure)
+                if (!pure && !nd_free)
                     found = probe_lane<LOG_SLOTS>(tab, (uint32_t)leaf.lo, (uint32_t)(leaf.lo >> 32), leaf.hi, leaf.k3, slot);
                 BG_T1(12, tp);
             }
+            if (nd_free) { commit(0ull, leaf, enc, slot, len, __ballot(valid && pure)); continue; }
             commit<true>(__ballot(valid && !pure && !found), leaf, enc, slot, len, __ballot(valid && pure));
             if (ovf) return;
         }
@@ -582,6 +610,30 @@ struct Gen {
     // checker on (a != dst(B)) commutes (the argument of canon_mask with the dice
     // swapped): (A, B) is a pass-1 two-step, already inserted, so only chain moves
     // and bar entries / bear-offs are walked.
+    // Without bar entries or bear-offs (nd_both: root not on the bar, >= 2
+    // checkers off the home board) the only two-steps that can coincide move ONE
+    // checker from c by hi + lo (s = the mover's direction):
+    //   chain     (c, hi)(c+s.hi, lo), pass 1   hits: c+s.hi, c+s(hi+lo) if blots
+    //   reverse   (c+s.lo, hi)(c, lo), pass 1   valid iff the root has a checker on
+    //                                           c+s.lo (so no blot there); hits: c+s(hi+lo)
+    //   pass-2    (c, lo)(c+s.lo, hi)           hits: c+s.lo, c+s(hi+lo)
+    // (every other two-step changes the counts without cancelling: unique).  The
+    // reverse one equals the pass-2 one whenever it exists, and the chain equals
+    // the reverse one iff c+s.hi is no blot, the pass-2 one iff neither c+s.hi nor
+    // c+s.lo is.  Walk order: PLAYER1 chain < reverse < pass-2 (first sub-move c <
+    // c+lo), PLAYER2 reverse < chain < pass-2.  Returns whether the entry of kind
+    // `kind` (1 chain, 2 reverse, 3 pass-2) is the first of its equals -- the one
+    // the reference keeps -- with the chain's validity (c+s.hi not blocked).
+    __device__ __forceinline__ bool nd_first(int c, int kind, int lo, int hi) const {
+        const int sg = pl == 0 ? 1 : -1, ph = c + sg * hi, pl_ = c + sg * lo;
+        const bool rev_ok = (root_occ >> pl_) & 1u;
+        const bool chain_ok = !((blocked >> ph) & 1u);
+        const bool hblot = (root_blot >> ph) & 1u, lblot = (root_blot >> pl_) & 1u;
+        if (kind == 1) return pl == 0 || !(rev_ok && !hblot);
+        if (kind == 2) return pl == 1 || !(chain_ok && !hblot);
+        return !rev_ok && !(chain_ok && !hblot && !lblot);
+    }
+
     __device__ __forceinline__ void nd_both(const Node& s0, int hi, int lo) {
         const int l = threadIdx.x & 63;
         const bool up = l >= 32;
@@ -606,9 +658,14 @@ struct Gen {
             if (up && a1 && bit < 24) q2 &= (1u << 31) | (1u << (pl == 0 ? bit + da : bit - da));
             uint64_t par = __ballot(a1 && q2 != 0u);
             if (!(two >> 32)) par &= kLow;
+            nd_free = (s0.k3 & 15u) == 0u && 15 - s0.n_home - (int)((s0.k3 >> 4) & 15u) >= 2;
+            if (nd_free) { root_occ = s0.occ; root_blot = s0.blot; }
+            else need_table();
             flat_leaves(par, t1, q2, x2, (uint64_t)e1, lo, 16, 2, hi);
+            nd_free = false;
             return;
         }
+        need_table();
         batch(a1 && !up, t1, (uint64_t)e1, 1);                  // pass 1: singles
         if (ovf || (n_unique == 1 && cur_max == 1)) return;     // :41-53
         if (two) flat_leaves(two, t1, q2, x2, (uint64_t)e1, hi, 16, 2);
@@ -754,6 +811,7 @@ struct Gen {
         // (bar included; 15 - home - off, which only over-counts a short board)
         pure_walk = 15 - s0.n_home - (int)((s0.k3 >> 4) & 15u) > 3 && (pl == 0 || Sink::kSet);
         mirror = pure_walk && pl == 1;
+        if (!pure_walk) need_table();
         // q*: a node's child list (dead-end test); c*: the children the walk
         // visits (canon_mask of the node's own child bit, which is its lane here)
         const Kids k1 = gen(s0, d, pl, blocked);
@@ -832,20 +890,20 @@ struct Gen {
 
     // non-doubles only (r0 != r1): the same as run() without the doubles code
     __device__ __forceinline__ void run_nd(const Node& s0, int r0, int r1) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; nd_free = false;
         const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
         nd_both(s0, hi, lo);
     }
 
     // doubles only (r0 == r1 == d)
     __device__ __forceinline__ void run_d(const Node& s0, int d) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; nd_free = false;
         doubles(s0, d);
     }
 
     // get_all_possible_moves (get_all_moves.py:9-70)
     __device__ __forceinline__ void run(const Node& s0, int r0, int r1) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; nd_free = false;
         if (r0 != r1) {
             const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
             nd_both(s0, hi, lo);

@@ -210,15 +210,8 @@ __device__ __forceinline__ int predict_class(int bv, uint64_t ctr, const Args& A
 template <int LOG, typename SlotPtr, int MEMO_KIND = 0, bool NO_DOUBLES = false>
 __device__ __forceinline__ int run_movegen(int bv, int pl, int r0, int r1, uint64_t* out, int cap, SlotPtr tab,
                                            int cap_unique, int* total, bool* ovf, uint4* memo) {
-    constexpr int slots = 1 << LOG;
-    for (int i = lane_id(); i < slots; i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = r0 == r1;
-    if (memo && dbl && MEMO_KIND != 2) {
-        constexpr int n = MEMO_KIND == 1 ? (1 << kLogCMemo) : kMemoSlots;
-        for (int i = lane_id(); i < n; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    Gen<LOG, SlotPtr, MoveSink, MEMO_KIND> g;
+    Gen<LOG, SlotPtr, MoveSink, MEMO_KIND> g;       // clears its table (and memo) when needed
     g.tab = tab; g.sink.out = out; g.sink.cap = cap; g.pl = pl; g.cap_unique = cap_unique;
     g.memo2 = memo && dbl ? memo : nullptr;
     g.memo3 = memo && dbl ? (MEMO_KIND != 0 ? memo : memo + (1 << kLogMemo2)) : nullptr;

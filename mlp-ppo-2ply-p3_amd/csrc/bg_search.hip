@@ -202,13 +202,8 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, int r, int q, cons
                                         unsigned long long& leaves) {
     const int r0 = kRoll0[r], r1 = kRoll1[r];
     const int l = lane_id();
-    for (int i = l; i < (1 << LOG); i += 64) tab[i] = make_uint4(0u, 0u, 0u, 0u);
     const bool dbl = KIND == 1 || (KIND == 2 && r0 == r1);
-    constexpr int kMemoN = MK == 1 ? (1 << kLogCMemo) : kMemoSlots;
-    if ((MK == 0 || MK == 1) && dbl)
-        for (int i = l; i < kMemoN; i += 64) memo[i] = make_uint4(0u, 0u, 0u, 0u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    Gen<LOG, SlotPtr, KeySink, MK < 0 ? 0 : MK> g;
+    Gen<LOG, SlotPtr, KeySink, MK < 0 ? 0 : MK> g;     // clears its table (and memo) when needed
     g.tab = tab; g.pl = q; g.cap_unique = cap_unique; g.blocked = blocked;
     if (MK == 2) memo = (uint4*)tab;    // non-null: pruning on (entries live in tab)
     g.memo2 = MK >= 0 && dbl && (S.memo_mask & 1) ? memo : nullptr;
