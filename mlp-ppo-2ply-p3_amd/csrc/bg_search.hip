@@ -57,9 +57,19 @@ constexpr int kMaxRounds = 256;
 // get_all_dice_rolls_tensor (get_all_dice_rolls.py:5-34): (1,1),(1,2),...,(6,6)
 __constant__ uint8_t kRoll0[21] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6};
 __constant__ uint8_t kRoll1[21] = {1, 2, 3, 4, 5, 6, 2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6, 6};
-// roll indices of the 15 non-doubles and the 6 doubles
-__constant__ uint8_t kNdRoll[15] = {1, 2, 3, 4, 5, 7, 8, 9, 10, 12, 13, 14, 16, 17, 19};
-__constant__ uint8_t kDbRoll[6] = {0, 6, 11, 15, 18, 20};
+// The same in arithmetic (the enumerators' per-job path: a table read there is a
+// dependent global load per job): roll r starts its first die's run at
+// 7(r0-1) - (r0-1)r0/2; the 15 non-doubles in order as nibbles.
+__host__ __device__ constexpr int roll_start(int r0) { return 7 * (r0 - 1) - (r0 - 1) * r0 / 2; }
+__device__ __forceinline__ void roll_dice(int r, int& r0, int& r1) {
+    r0 = 1 + (r >= 6) + (r >= 11) + (r >= 15) + (r >= 18) + (r >= 20);
+    r1 = r - roll_start(r0) + r0;
+}
+constexpr uint64_t kNdR0 = 0x544333222211111ull, kNdR1 = 0x665654654365432ull;
+__device__ __forceinline__ int nd_roll(int k) {     // k-th non-doubles roll index
+    const int a = (int)((kNdR0 >> (4 * k)) & 15u), b = (int)((kNdR1 >> (4 * k)) & 15u);
+    return roll_start(a) + b - a;
+}
 
 // Value net packed for MFMA (bgx_value_pack), in floats (H <= 128):
 //                         hdr [4] (e1 as int bits), then NT = ceil(H/16) tiles of
@@ -200,7 +210,8 @@ template <int LOG, typename SlotPtr, int MK, int KIND>
 __device__ __forceinline__ int enum_job(const S2& S, int job, int r, int q, const Node& sq, uint32_t blocked,
                                         SlotPtr tab, int cap_unique, uint4* memo, KeySink& sink,
                                         unsigned long long& leaves) {
-    const int r0 = kRoll0[r], r1 = kRoll1[r];
+    int r0, r1;
+    roll_dice(r, r0, r1);
     const int l = lane_id();
     const bool dbl = KIND == 1 || (KIND == 2 && r0 == r1);
     Gen<LOG, SlotPtr, KeySink, MK < 0 ? 0 : MK> g;     // clears its table (and memo) when needed
@@ -295,7 +306,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             constexpr int nr = VARIANT == 0 ? 15 : 6;
             #pragma unroll 1
             for (int k = 0; k < nr; ++k) {
-                const int r = VARIANT == 0 ? kNdRoll[k] : kDbRoll[k];
+                const int r = VARIANT == 0 ? nd_roll(k) : roll_start(k + 1);
                 const int job = row * 21 + r;
                 done(enum_job<LOG, uint4*, MK, VARIANT>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves), job);
             }
@@ -989,9 +1000,11 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             const char* c = strchr(hv, ':');
             if (c) { hmk = atoi(c + 1); c = strchr(c + 1, ':'); if (c) hwpe = atoi(c + 1); }
         }
-        void (*kheavy)(S2) = k_enum<9, 2, 1>;
-        void (*klist)(S2) = k_enum<9, 2, 2>;
+        // occupancy floor: <= 128 VGPRs (4 waves/SIMD) for the doubles walk (+1.5 %)
+        void (*kheavy)(S2) = k_enum<9, 2, 1, 4>;
+        void (*klist)(S2) = k_enum<9, 2, 2, 4>;
         if (hlog == 9 && hmk == 0) { kheavy = k_enum<9, 0, 1>; klist = k_enum<9, 0, 2>; }
+        else if (hlog == 9 && hmk == 2 && hwpe == 1) { kheavy = k_enum<9, 2, 1, 1>; klist = k_enum<9, 2, 2, 1>; }
         else if (hlog == 9 && hmk == 2 && hwpe == 5) { kheavy = k_enum<9, 2, 1, 5>; klist = k_enum<9, 2, 2, 5>; }
         else if (hlog == 9 && hmk == 2 && hwpe == 6) { kheavy = k_enum<9, 2, 1, 6>; klist = k_enum<9, 2, 2, 6>; }
         else if (hlog == 8 && hmk == 2) { kheavy = k_enum<8, 2, 1>; klist = k_enum<8, 2, 2>; }
@@ -1010,7 +1023,11 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const float* f16s = vpacked;
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4, value_bias};
-        int g_light = persistent_grid(e, k_enum<kLogLight, -1, 0>, 32);
+        // BGX_2PLY_LWPE=8: the non-doubles enumerator held to 64 VGPRs (A/B; it spills
+        // and runs slower than at 75 VGPRs / 6 waves per SIMD)
+        const char* lw = getenv("BGX_2PLY_LWPE");
+        void (*klight)(S2) = lw && atoi(lw) == 8 ? k_enum<kLogLight, -1, 0, 8> : k_enum<kLogLight, -1, 0, 1>;
+        int g_light = persistent_grid(e, klight, 32);
         int g_heavy = persistent_grid(e, kheavy, 32);
         if (const char* v = getenv("BGX_2PLY_HGRID")) g_heavy = atoi(v) > 0 ? atoi(v) : g_heavy;
         if (const char* v = getenv("BGX_2PLY_LGRID")) g_light = atoi(v) > 0 ? atoi(v) : g_light;
@@ -1072,12 +1089,12 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
                     SCK(hipEventRecord(e->search_ev[3], s));
                     SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
                     hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, e->search_side, S);
+                    hipLaunchKernelGGL(klight, dim3(g_light), dim3(64), 0, e->search_side, S);
                     SCK(hipEventRecord(e->search_ev[4], e->search_side));
                     SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
                 } else {
                     hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                    hipLaunchKernelGGL((k_enum<kLogLight, -1, 0>), dim3(g_light), dim3(64), 0, s, S);
+                    hipLaunchKernelGGL(klight, dim3(g_light), dim3(64), 0, s, S);
                 }
                 tiers();
                 SCK(hipEventRecord(e->search_ev[1], s));
