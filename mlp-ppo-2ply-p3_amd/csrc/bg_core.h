@@ -438,10 +438,26 @@ struct Gen {
     bool ovf;
     bool pure_walk = false;   // this doubles walk visits every state once: no table, no memo
     bool mirror = false;      // ... in PLAYER2's mirrored order (set semantics only)
+    bool forbid = false;      // ... PLAYER2, ordered: forbidden-point masks (kids())
     bool nd_free = false;     // nd_both's two-steps decided without the table (flat_leaves)
     bool clean = false;       // table (and memo) cleared for this run: callers leave it
                               // dirty and the walk clears it only if it needs it
     uint32_t root_occ = 0, root_blot = 0;
+
+    // The children a walk visits below a sub-move with child bit `bit` that led
+    // from node `from` to node `t` (q = t's child list, F = the forbidden points
+    // above it).  forbid (PLAYER2 walks without bear-off, ordered semantics): the
+    // walk visits the reference's smallest-key path of every state exactly once --
+    // a point below an earlier sub-move's source that was occupied when that
+    // sub-move was made could have moved first, in the smaller order, so it is
+    // forbidden from then on (F grows by from.occ below bit; tools/check_canon.py
+    // checks the lists against the oracle).  Otherwise canon_mask.
+    __device__ __forceinline__ uint32_t kids(uint32_t q, int bit, int d, const Node& from, const Node& t,
+                                             uint32_t& F) const {
+        if (!forbid) return q & canon_mask(bit, d, pl, t, mirror);
+        if (bit < 24) F |= from.occ & ((1u << bit) - 1u);
+        return q & ~F;
+    }
 
     // clear the dedup table and the separate memo tables before first use
     __device__ __forceinline__ void need_table() {
@@ -709,7 +725,7 @@ struct Gen {
     // the lanes in `parents` (lane order = DFS order), 64 at a time, the revisit
     // check (first in lane order wins) and each chunk's leaves as one flat batch.
     __device__ __forceinline__ void flat_depth3(uint64_t parents, const Node& t2, uint32_t q3, int x3, uint64_t penc2,
-                                                int d) {
+                                                int d, uint32_t F2) {
         const int l = threadIdx.x & 63;
         const bool par = (parents >> l) & 1ull;
         const uint32_t cnt = par ? (uint32_t)__popc(q3) : 0u;
@@ -732,6 +748,7 @@ struct Gen {
             const Kids k{qb, __shfl(x3, src)};
             const uint64_t pe = !Sink::kEnc ? 0ull : (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc2, src) |
                                 ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(penc2 >> 32), src) << 32);
+            uint32_t F3 = forbid ? (uint32_t)__shfl((int)F2, src) : 0u;
             Node t3;
             uint64_t pe3 = 0;
             int cb = 31;
@@ -744,7 +761,7 @@ struct Gen {
             const uint64_t f3 = memo_batch<kLogMemo3, true>(memo3, n_memo3, valid, t3, kTag3);
             uint32_t q4 = 0;
             int x4 = -1;
-            if ((f3 >> l) & 1ull) { const Kids kk = gen(t3, d, pl, blocked); q4 = kk.bits & canon_mask(cb, d, pl, t3, mirror); x4 = kk.extra; }
+            if ((f3 >> l) & 1ull) { const Kids kk = gen(t3, d, pl, blocked); q4 = kids(kk.bits, cb, d, s2, t3, F3); x4 = kk.extra; }
             flat_leaves(__ballot(((f3 >> l) & 1ull) && q4 != 0u), t3, q4, x4, pe3, d, 48, 4);
             if (ovf) return;
         }
@@ -753,7 +770,7 @@ struct Gen {
     // The same one level up: the depth-2 children of the depth-1 nodes on the
     // lanes in `parents`, 64 at a time, revisit check, then flat_depth3 per chunk.
     __device__ __forceinline__ void flat_depth2(uint64_t parents, const Node& t1, uint32_t q2, int x2, uint64_t penc1,
-                                                int d) {
+                                                int d, uint32_t F1) {
         const int l = threadIdx.x & 63;
         const bool par = (parents >> l) & 1ull;
         const uint32_t cnt = par ? (uint32_t)__popc(q2) : 0u;
@@ -775,6 +792,7 @@ struct Gen {
             const Node s1 = shfl_node(t1, src);
             const Kids k{qb, __shfl(x2, src)};
             const uint64_t pe = !Sink::kEnc ? 0ull : (uint64_t)(uint32_t)__shfl((int)(uint32_t)penc1, src);
+            uint32_t F2 = forbid ? (uint32_t)__shfl((int)F1, src) : 0u;
             Node t2;
             uint64_t pe2 = 0;
             int cb = 31;
@@ -787,8 +805,8 @@ struct Gen {
             const uint64_t f2 = memo_batch<kLogMemo2, true>(memo2, n_memo2, valid, t2, kTag2);
             uint32_t q3 = 0;
             int x3 = -1;
-            if ((f2 >> l) & 1ull) { const Kids kk = gen(t2, d, pl, blocked); q3 = kk.bits & canon_mask(cb, d, pl, t2, mirror); x3 = kk.extra; }
-            flat_depth3(__ballot(((f2 >> l) & 1ull) && q3 != 0u), t2, q3, x3, pe2, d);
+            if ((f2 >> l) & 1ull) { const Kids kk = gen(t2, d, pl, blocked); q3 = kids(kk.bits, cb, d, s1, t2, F2); x3 = kk.extra; }
+            flat_depth3(__ballot(((f2 >> l) & 1ull) && q3 != 0u), t2, q3, x3, pe2, d, F2);
             if (ovf) return;
         }
     }
@@ -809,8 +827,9 @@ struct Gen {
         const int l = threadIdx.x & 63;
         // no bear-off within 4 sub-moves: more than 3 checkers off the home board
         // (bar included; 15 - home - off, which only over-counts a short board)
-        pure_walk = 15 - s0.n_home - (int)((s0.k3 >> 4) & 15u) > 3 && (pl == 0 || Sink::kSet);
-        mirror = pure_walk && pl == 1;
+        pure_walk = 15 - s0.n_home - (int)((s0.k3 >> 4) & 15u) > 3;
+        mirror = pure_walk && pl == 1 && Sink::kSet;
+        forbid = pure_walk && pl == 1 && !Sink::kSet;
         if (!pure_walk) need_table();
         // q*: a node's child list (dead-end test); c*: the children the walk
         // visits (canon_mask of the node's own child bit, which is its lane here)
@@ -820,10 +839,11 @@ struct Gen {
         const bool a1 = lane_child(s0, k1, d, t1, e1);
         uint32_t q2 = 0, c2 = 0;
         int x2 = -1;
-        if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; c2 = q2 & canon_mask(l, d, pl, t1, mirror); x2 = k.extra; }
+        uint32_t F1 = 0;       // forbidden points below each node (forbid mode)
+        if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; c2 = kids(q2, l, d, s0, t1, F1); x2 = k.extra; }
         for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
             if (got4) {
-                flat_depth2((uint64_t)b1 & __ballot(c2 != 0u), t1, c2, x2, (uint64_t)e1, d);
+                flat_depth2((uint64_t)b1 & __ballot(c2 != 0u), t1, c2, x2, (uint64_t)e1, d, F1);
                 return;
             }
             const int i1 = __builtin_ctz(b1);
@@ -841,10 +861,11 @@ struct Gen {
             BG_CNT(3, __popcll(f2));
             uint32_t q3 = 0, c3 = 0;
             int x3 = -1;
-            if ((f2 >> l) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; c3 = q3 & canon_mask(l, d, pl, t2, mirror); x3 = k.extra; }
+            uint32_t F2 = forbid ? rdl(F1, i1) : 0u;
+            if ((f2 >> l) & 1ull) { const Kids k = gen(t2, d, pl, blocked); q3 = k.bits; c3 = kids(q3, l, d, s1, t2, F2); x3 = k.extra; }
             for (uint64_t b2 = f2; b2; b2 &= b2 - 1ull) {
                 if (got4) {
-                    flat_depth3(b2 & __ballot(c3 != 0u), t2, c3, x3, m1 | ((uint64_t)e2l << 16), d);
+                    flat_depth3(b2 & __ballot(c3 != 0u), t2, c3, x3, m1 | ((uint64_t)e2l << 16), d, F2);
                     if (ovf) return;
                     break;
                 }
@@ -863,7 +884,8 @@ struct Gen {
                 BG_CNT(5, __popcll(f3));
                 uint32_t q4 = 0, c4 = 0;
                 int x4 = -1;
-                if ((f3 >> l) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; c4 = q4 & canon_mask(l, d, pl, t3, mirror); x4 = k.extra; }
+                uint32_t F3 = forbid ? rdl(F2, i2) : 0u;
+                if ((f3 >> l) & 1ull) { const Kids k = gen(t3, d, pl, blocked); q4 = k.bits; c4 = kids(q4, l, d, s2, t3, F3); x4 = k.extra; }
                 for (uint64_t b3 = f3; b3; b3 &= b3 - 1ull) {
                     const int i3 = __ffsll((unsigned long long)b3) - 1;
                     if (!rdl(q4, i3)) {
@@ -890,20 +912,20 @@ struct Gen {
 
     // non-doubles only (r0 != r1): the same as run() without the doubles code
     __device__ __forceinline__ void run_nd(const Node& s0, int r0, int r1) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; nd_free = false;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; forbid = false; nd_free = false;
         const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
         nd_both(s0, hi, lo);
     }
 
     // doubles only (r0 == r1 == d)
     __device__ __forceinline__ void run_d(const Node& s0, int d) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; nd_free = false;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; forbid = false; nd_free = false;
         doubles(s0, d);
     }
 
     // get_all_possible_moves (get_all_moves.py:9-70)
     __device__ __forceinline__ void run(const Node& s0, int r0, int r1) {
-        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; nd_free = false;
+        cur_max = 0; count = 0; n_unique = 0; ovf = false; n_memo2 = 0; n_memo3 = 0; pure_walk = false; mirror = false; forbid = false; nd_free = false;
         if (r0 != r1) {
             const int hi = r0 > r1 ? r0 : r1, lo = r0 > r1 ? r1 : r0;
             nd_both(s0, hi, lo);

@@ -74,13 +74,18 @@ def enc(src, dst, hit):
     return s | (t << 5) | (hit << 10) | 0x8000
 
 
-def children(b, d, pl, last, mirror=False):
+def children(b, d, pl, last, mirror=False, forbid=None):
     """(bit, src, dst) in DFS order, canonical after a sub-move with bit `last`.
-    mirror (PLAYER2, set semantics only): bits <= last instead."""
+    mirror (PLAYER2, set semantics only): bits <= last instead.
+    forbid (PLAYER2 walks without bear-off, ordered): the points below an earlier
+    sub-move's source that were occupied when it was made."""
     srcs, special = gen(b, d, pl)
     out = []
     for s in srcs:
-        if last is not None and last < 24:
+        if forbid is not None:
+            if (forbid >> s) & 1:
+                continue
+        elif last is not None and last < 24:
             if mirror:
                 if s > last:
                     continue
@@ -95,12 +100,15 @@ def children(b, d, pl, last, mirror=False):
     return out
 
 
-def walk(b0, d, pl, mirror=False):
+def walk(b0, d, pl, mirror=False, use_forbid=False):
     inserts = []          # (key bytes, encoded move, len) in walk order
     got4 = [False]
 
-    def rec(b, depth, last, code):
-        kids = children(b, d, pl, last, mirror) if depth < 4 else []
+    def occ(b):
+        return sum(1 << i for i in range(24) if b[pl * 24 + i] > 0)
+
+    def rec(b, depth, last, code, forbid=0):
+        kids = children(b, d, pl, last, mirror, forbid if use_forbid else None) if depth < 4 else []
         has_kids = bool(gen(b, d, pl)[0]) or gen(b, d, pl)[1] is not None
         if depth == 4 or (not has_kids and depth > 0):
             if depth == 4 or not got4[0]:
@@ -110,7 +118,8 @@ def walk(b0, d, pl, mirror=False):
             return
         for bit, s, t in kids:
             nb, hit = apply(b, s, t, pl)
-            rec(nb, depth + 1, bit, code | (enc(s, t, hit) << (16 * depth)))
+            nf = forbid | (occ(b) & ((1 << bit) - 1)) if bit < 24 else forbid
+            rec(nb, depth + 1, bit, code | (enc(s, t, hit) << (16 * depth)), nf)
 
     rec(b0, 0, None, 0)
     seen, out = set(), []
@@ -159,6 +168,12 @@ def check(n, seed=11):
                 keys = [k for k, _, _ in inserts]
                 assert len(keys) == len(set(keys)), (i, b.tolist(), pl, d)
             else:
+                # PLAYER2, ordered: the forbidden-point walk visits each state once,
+                # first occurrences in the reference's order
+                got_f, fins = walk(b, d, pl, use_forbid=True)
+                keys = [k for k, _, _ in fins]
+                assert len(keys) == len(set(keys)), ("forbid", i, b.tolist(), pl, d)
+                assert [int(v) for v in ref] == got_f, ("forbid", i, b.tolist(), pl, d)
                 # PLAYER2, set semantics (2-ply): the mirrored walk visits each
                 # state once and yields the same set of afterstates
                 _, mins = walk(b, d, pl, mirror=True)
