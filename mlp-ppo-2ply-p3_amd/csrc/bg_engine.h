@@ -393,8 +393,9 @@ __device__ __forceinline__ void store_rec(const Args& A, int gi, int bv) { A.lan
 // Engine object behind the C ABI's opaque bgx_engine*.
 struct bgx_engine {
     int device;
-    int lds_log;      // 9, 10 or 11
-    int memo_mode;    // 1: separate memo tables, 2: memo inside the dedup table
+    int lds_log;      // 8 .. 11 (the split's doubles prefix; standalone movegen 9 .. 11)
+    int memo_mode;    // 0: none, 1: separate memo tables, 2: memo inside the dedup table
+    int heavy_wpe;    // 5: the doubles prefix held to 5 waves/SIMD (A/B)
     bool split;       // Philox mode: doubles-prefix launch, then the light launch
     bg::Args a;
     uint4* slow_tables;

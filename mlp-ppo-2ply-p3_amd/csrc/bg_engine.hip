@@ -57,8 +57,8 @@ __device__ __forceinline__ void step_lane(const Args& A, int gi, uint4* tab, uin
 // `base` offsets blockIdx into the dispatch order.  MEMO: 0 = no revisit memo,
 // 1 = separate memo tables (10 KB of LDS), 2 = memo inside the dedup table.
 // NO_DOUBLES: doubles rolls are deferred to the overflow tiers (light launch).
-template <int PHASE, int LOG, int MEMO = 1, bool NO_DOUBLES = false>
-__global__ __launch_bounds__(64) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
+template <int PHASE, int LOG, int MEMO = 1, bool NO_DOUBLES = false, int WPE = 1>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_step(Args A, const int32_t* actions, float* obs, float* reward, uint8_t* done,
                                              int32_t* info, int base) {
     __shared__ uint4 tab[1 << LOG];
     __shared__ uint4 memo_[MEMO == 1 ? kMemoSlots : 1];
@@ -483,6 +483,24 @@ static void launch_order(bgx_engine* e, hipStream_t s) {
 static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, const int32_t* actions, float* obs,
                         float* reward, uint8_t* done, int32_t* info, int base = 0) {
     if (grid <= 0) return;
+#define STEP_K(...) hipLaunchKernelGGL((k_step<__VA_ARGS__>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, \
+                                       info, base)
+    // default (the split's doubles prefix): a 512-slot table and no revisit memo
+    // (8 KB of LDS): the doubles walks that cannot bear off use no table at all,
+    // so occupancy (VGPR-bound, 4 waves/SIMD) beats a bigger table (C3: 1,024
+    // slots + memo 242 M/s, 512 slots + memo inside 284 M/s, no memo 288 M/s)
+    if (e->memo_mode == 2 && e->lds_log == 9) {
+        if (e->heavy_wpe == 5) STEP_K(0, 9, 2, false, 5);
+        else STEP_K(0, 9, 2);
+        return;
+    }
+    if (e->memo_mode == 2 && e->lds_log == 8) { STEP_K(0, 8, 2); return; }
+    if (e->memo_mode == 0) {
+        if (e->lds_log == 8) STEP_K(0, 8, 0);
+        else STEP_K(0, 9, 0);
+        return;
+    }
+#undef STEP_K
     if (e->memo_mode == 2) {
         if (e->lds_log == 11)
             hipLaunchKernelGGL((k_step<0, 11, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
@@ -540,14 +558,16 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     e->device = device;
     e->seed = seed;
     const char* ll = getenv("BGX_LDS_LOG");
-    e->lds_log = ll ? atoi(ll) : 10;
-    if (e->lds_log < 9 || e->lds_log > 11) e->lds_log = 10;
+    e->lds_log = ll ? atoi(ll) : 9;
+    if (e->lds_log < 8 || e->lds_log > 11) e->lds_log = 9;
+    const char* hw = getenv("BGX_HEAVY_WPE");
+    e->heavy_wpe = hw ? atoi(hw) : 1;
     const char* sp = getenv("BGX_SPLIT");
     e->split = !(sp && sp[0] == '0');
     const char* sov = getenv("BGX_STEP_OVERLAP");
     e->step_overlap = sov ? atoi(sov) : 1;
     const char* mm = getenv("BGX_MEMO_MODE");
-    e->memo_mode = mm ? atoi(mm) : 1;
+    e->memo_mode = mm ? atoi(mm) : 0;
     Args& A = e->a;
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
