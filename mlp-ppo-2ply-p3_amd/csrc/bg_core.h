@@ -423,6 +423,18 @@ struct MoveSink {
 // and bar + off + sum(counts) = 15 keeps the depth-2 and depth-3 images apart).
 constexpr uint32_t kTag2 = 0xFFFFFF00u, kTag3 = 0xFFFFFF0Fu;
 
+// Gen::nd_first as a free function (also the 2-ply's row-level non-doubles walk)
+__device__ __forceinline__ bool nd_first_of(int c, int kind, int lo, int hi, int pl, uint32_t root_occ,
+                                            uint32_t root_blot, uint32_t blocked) {
+    const int sg = pl == 0 ? 1 : -1, ph = c + sg * hi, pl_ = c + sg * lo;
+    const bool rev_ok = (root_occ >> pl_) & 1u;
+    const bool chain_ok = !((blocked >> ph) & 1u);
+    const bool hblot = (root_blot >> ph) & 1u, lblot = (root_blot >> pl_) & 1u;
+    if (kind == 1) return pl == 0 || !(rev_ok && !hblot);
+    if (kind == 2) return pl == 1 || !(chain_ok && !hblot);
+    return !rev_ok && !(chain_ok && !hblot && !lblot);
+}
+
 template <int LOG_SLOTS, typename SlotPtr, typename Sink = MoveSink, int MEMO_KIND = 0>
 struct Gen {
     static constexpr bool TAGGED = MEMO_KIND == 2;
@@ -641,13 +653,7 @@ struct Gen {
     // `kind` (1 chain, 2 reverse, 3 pass-2) is the first of its equals -- the one
     // the reference keeps -- with the chain's validity (c+s.hi not blocked).
     __device__ __forceinline__ bool nd_first(int c, int kind, int lo, int hi) const {
-        const int sg = pl == 0 ? 1 : -1, ph = c + sg * hi, pl_ = c + sg * lo;
-        const bool rev_ok = (root_occ >> pl_) & 1u;
-        const bool chain_ok = !((blocked >> ph) & 1u);
-        const bool hblot = (root_blot >> ph) & 1u, lblot = (root_blot >> pl_) & 1u;
-        if (kind == 1) return pl == 0 || !(rev_ok && !hblot);
-        if (kind == 2) return pl == 1 || !(chain_ok && !hblot);
-        return !rev_ok && !(chain_ok && !hblot && !lblot);
+        return nd_first_of(c, kind, lo, hi, pl, root_occ, root_blot, blocked);
     }
 
     __device__ __forceinline__ void nd_both(const Node& s0, int hi, int lo) {

@@ -196,6 +196,30 @@ struct KeySink {
     __device__ __forceinline__ void push(const Node& s, uint64_t enc, int idx, int len) {
         push_lanes(1ull, s, enc, idx, len);
     }
+    // push_lanes with the job given per lane (the row-level walk, nd_row)
+    __device__ __forceinline__ void push_lanes_job(uint64_t m, const Node& t, uint32_t job_lane, int len) {
+        if (lost) return;
+        const int n = __popcll(m);
+        const int l = threadIdx.x & 63;
+        const bool on = (m >> l) & 1ull;
+        int p = fill + lane_rank(m);
+        unsigned long long b = blk;
+        if (fill + n > kBlk) {
+            unsigned long long nb = 0;
+            if (l == 0) nb = atomicAdd(cursor, (unsigned long long)kBlk);
+            nb = bcast64(nb);
+            if (nb + kBlk > cap) { lost = true; return; }
+            if (p >= kBlk) { b = nb; p -= kBlk; }
+            blk = nb;
+            fill = fill + n - kBlk;
+        } else {
+            fill += n;
+        }
+        if (on) {
+            keys[b + p] = make_uint4((uint32_t)t.lo, (uint32_t)(t.lo >> 32), t.hi, t.k3);
+            tags[b + p] = job_lane | ((uint32_t)len << 29);
+        }
+    }
     // mark the unused tail of the wave's current block
     __device__ __forceinline__ void finish() {
         for (int i = fill + (threadIdx.x & 63); i < kBlk; i += 64) tags[blk + i] = kTagNone;
@@ -235,6 +259,123 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, int r, int q, cons
     return 0;
 }
 
+// All 15 non-doubles rolls of one row in one pass (the 2-ply's set semantics):
+// the first sub-moves of all six dice on the lanes (die d_l, source a_l), each
+// lane's second-level child lists for the five other dice, then the two-steps of
+// every roll as flat 64-lane chunks, one per second die -- instead of 15 jobs that
+// each rebuild two first levels and run their own chunks.  Only for rows without
+// bar entries or bear-offs (no bar, >= 2 checkers off the home board), where
+// Gen::nd_both decides every two-step without a table (pure, or the first of a
+// chain / reverse / pass-2 family: nd_first_of); a roll whose pass 1 has no
+// two-step (the sequential singles semantics), and every roll of any other row,
+// is left to the per-job walk.  Returns the mask of roll indices (0..20) left.
+__device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0, int q, uint32_t blocked,
+                                           KeySink& sink, unsigned long long& leaves) {
+    constexpr uint32_t kAllNd = 0x000B77BEu;        // the 15 non-doubles roll indices
+    const int off = (int)((s0.k3 >> 4) & 15u);
+    if ((s0.k3 & 15u) != 0u || 15 - s0.n_home - off < 2) return kAllNd;
+    const int l = lane_id();
+    uint32_t K[7];
+    int st[8];
+    st[1] = 0;
+    #pragma unroll
+    for (int d = 1; d <= 6; ++d) {
+        K[d] = gen(s0, d, q, blocked).bits;
+        st[d + 1] = st[d] + __popc(K[d]);
+    }
+    const int n1 = st[7];
+    if (n1 > 64) return kAllNd;
+    // lane l: first sub-move (die dl, source al)
+    const bool act = l < n1;
+    int dl = 1;
+    #pragma unroll
+    for (int d = 2; d <= 6; ++d) dl = l >= st[d] ? d : dl;
+    uint32_t kd = K[1];
+    #pragma unroll
+    for (int d = 2; d <= 6; ++d) kd = dl == d ? K[d] : kd;
+    int kst = 0;
+    #pragma unroll
+    for (int d = 1; d <= 6; ++d) kst = dl == d ? st[d] : kst;
+    const int al = act ? select_bit(kd, l - kst) : 0;
+    Node t1 = s0;
+    uint32_t Q[7];
+    Q[0] = 0u;
+    if (act) {
+        const Kids k{kd, -1};
+        t1 = apply(s0, child(s0, k, al, dl, q), q);
+    }
+    #pragma unroll
+    for (int e = 1; e <= 6; ++e) Q[e] = act && e != dl ? gen(t1, e, q, blocked).bits : 0u;
+    // roll (hi, lo) is fast iff its pass 1 (hi first) has a two-step
+    uint64_t M[7], N[7];
+    #pragma unroll
+    for (int d = 1; d <= 6; ++d) { M[d] = __ballot(act && dl == d); N[d] = __ballot(Q[d] != 0u); }
+    uint32_t slow = 0u;
+    #pragma unroll
+    for (int hi = 2; hi <= 6; ++hi)
+        #pragma unroll
+        for (int lo = 1; lo < hi; ++lo)
+            if (!(M[hi] & N[lo])) slow |= 1u << (roll_start(lo) + hi - lo);
+    const int sg = q == 0 ? 1 : -1;
+    const uint32_t root_occ = s0.occ, root_blot = s0.blot;
+    const uint32_t job0 = (uint32_t)row * 21u;
+    unsigned long long emitted = 0;
+    #pragma unroll 1
+    for (int e = 1; e <= 6; ++e) {
+        // this lane's two-steps with second die e: pass 1 of roll (dl, e) if dl > e,
+        // pass 2 of roll (e, dl) if dl < e (only its chain child)
+        const int hi = dl > e ? dl : e, lo = dl > e ? e : dl;
+        const int r = roll_start(lo) + hi - lo;
+        uint32_t c = Q[e];
+        if (dl < e) c &= 1u << (al + sg * dl);
+        if (!act || dl == e || ((slow >> r) & 1u)) c = 0u;
+        const uint32_t cnt = (uint32_t)__popc(c);
+        uint32_t pre = 0, total = 0;
+        const uint64_t below = (1ull << l) - 1ull;
+        #pragma unroll
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t m = __ballot((cnt >> b) & 1u);
+            pre += (uint32_t)__popcll(m & below) << b;
+            total += (uint32_t)__popcll(m) << b;
+        }
+        const int meta = al | (dl << 5) | (r << 8);
+        for (uint32_t ch = 0; ch < total; ch += 64) {
+            const uint32_t pp = ch + (uint32_t)l;
+            const bool valid = pp < total;
+            const int src = parent_of(pp, pre + cnt);
+            const uint32_t qb = (uint32_t)__shfl((int)c, src);
+            const int j = (int)(pp - (uint32_t)__shfl((int)pre, src));
+            const Node s1 = shfl_node(t1, src);
+            const int mt = __shfl(meta, src);
+            const int pa = mt & 31, pd = (mt >> 5) & 7, pr = mt >> 8;
+            Node leaf = s1;
+            bool emit = false;
+            if (valid) {
+                const int cb = select_bit(qb, j);
+                const Kids k{qb, -1};
+                const Sub m = child(s1, k, cb, e, q);
+                leaf = apply(s1, m, q);
+                if (pd > e) {               // pass 1: (pa, hi = pd) then (cb, lo = e)
+                    const int dst_a = pa + sg * pd;
+                    const bool chain = cb == dst_a, rev = m.dst == pa;
+                    emit = (!chain && !rev) ||
+                           nd_first_of(chain ? pa : cb, chain ? 1 : 2, e, pd, q, root_occ, root_blot, blocked);
+                } else {                    // pass 2: (pa, lo = pd) then its chain (cb, hi = e)
+                    emit = nd_first_of(pa, 3, pd, e, q, root_occ, root_blot, blocked);
+                }
+            }
+            const uint64_t em = __ballot(valid && emit);
+            sink.push_lanes_job(em, leaf, job0 + (uint32_t)pr, 2);
+            emitted += (unsigned long long)__popcll(em);
+        }
+    }
+    // every fast roll has a first pass-1 two-step (emitted): max length 2
+    const uint32_t fast = kAllNd & ~slow;
+    if (l < 21 && ((fast >> l) & 1u) && !sink.lost) S.maxlen[job0 + (uint32_t)l] = 2;
+    if (!sink.lost) leaves += emitted;
+    return slow;
+}
+
 // The replier's node of row `row` (its 64-byte record, one byte per lane).
 __device__ __forceinline__ Node row_node(int bv, int& q, uint32_t& blocked) {
     q = rd(bv, 52);
@@ -269,7 +410,7 @@ __device__ __forceinline__ KeySink make_sink(const S2& S) {
 }
 
 // VARIANT 0: jobs (row, non-doubles roll) implicit, 1: (row, doubles roll)
-// implicit, 2: the explicit list.
+// implicit, 2: the explicit list, 3: as 0 with the row-level walk (nd_row) first.
 template <int LOG, int MK, int VARIANT, int WPE = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_enum(S2 S) {
     __shared__ uint4 tab[1 << LOG];
@@ -277,7 +418,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     uint4* memo = MK >= 0 ? memo_ : nullptr;
     KeySink sink = make_sink(S);
     unsigned long long leaves = 0;
-    const int cap = VARIANT == 0 ? S.cap_light : S.cap_heavy;
+    const int cap = VARIANT == 0 || VARIANT == 3 ? S.cap_light : S.cap_heavy;
     auto done = [&](int st, int job) {
         if (st == 1) {
             const int qo = LOG < 10 ? 0 : 1;
@@ -303,12 +444,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             int q;
             uint32_t blocked;
             const Node sq = row_node(bv, q, blocked);
-            constexpr int nr = VARIANT == 0 ? 15 : 6;
-            #pragma unroll 1
-            for (int k = 0; k < nr; ++k) {
-                const int r = VARIANT == 0 ? nd_roll(k) : roll_start(k + 1);
-                const int job = row * 21 + r;
-                done(enum_job<LOG, uint4*, MK, VARIANT>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves), job);
+            if (VARIANT == 3) {
+                // the row-level walk; what it leaves (and a lost pool block: the
+                // whole row again) runs per job
+                uint32_t left = nd_row(S, row, sq, q, blocked, sink, leaves);
+                if (sink.lost) left = 0x000B77BEu;
+                #pragma unroll 1
+                for (; left; left &= left - 1u) {
+                    const int r = __builtin_ctz(left);
+                    const int job = row * 21 + r;
+                    done(enum_job<LOG, uint4*, MK, 0>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves), job);
+                }
+            } else {
+                constexpr int nr = VARIANT == 0 ? 15 : 6;
+                #pragma unroll 1
+                for (int k = 0; k < nr; ++k) {
+                    const int r = VARIANT == 0 ? nd_roll(k) : roll_start(k + 1);
+                    const int job = row * 21 + r;
+                    done(enum_job<LOG, uint4*, MK, VARIANT>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves),
+                         job);
+                }
             }
             bv = bv_next;
         }
@@ -1026,7 +1181,10 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         // BGX_2PLY_LWPE=8: the non-doubles enumerator held to 64 VGPRs (A/B; it spills
         // and runs slower than at 75 VGPRs / 6 waves per SIMD)
         const char* lw = getenv("BGX_2PLY_LWPE");
-        void (*klight)(S2) = lw && atoi(lw) == 8 ? k_enum<kLogLight, -1, 0, 8> : k_enum<kLogLight, -1, 0, 1>;
+        // BGX_2PLY_ROWS=0: the per-job non-doubles walk only (A/B)
+        const char* rw = getenv("BGX_2PLY_ROWS");
+        void (*klight)(S2) = lw && atoi(lw) == 8 ? k_enum<kLogLight, -1, 0, 8>
+                             : (rw && rw[0] == '0') ? k_enum<kLogLight, -1, 0, 1> : k_enum<kLogLight, -1, 3, 1>;
         int g_light = persistent_grid(e, klight, 32);
         int g_heavy = persistent_grid(e, kheavy, 32);
         if (const char* v = getenv("BGX_2PLY_HGRID")) g_heavy = atoi(v) > 0 ? atoi(v) : g_heavy;
