@@ -182,15 +182,27 @@ __device__ __forceinline__ int lane_of_block(const Args& A, int bi) {
 
 constexpr int kClasses = 5;
 
+// Philox counters (the low 48 bits) carry in bits 48-63 the lane's next roll as
+// the previous step predicted it (predict_class): valid << 15 | r0 | r1 << 3 |
+// draws << 6.  The next normal roll takes it instead of running the same Philox
+// block again and advances the counter by the draws; a reset ignores it (it
+// draws from the counter as if nothing had been predicted), so the dice stream
+// is exactly the one without the cache.
+constexpr uint64_t kCtrMask = (1ull << 48) - 1ull;
+
 // Cost class of the lane's NEXT movegen (0 = heaviest).  Philox dice are a pure
 // function of (key, lane, counter), so the next roll is known now; the mover
 // after the next apply is 1 - cur.  Doubles dominate (a 4-deep DFS) and grow
 // with the number of points the mover occupies.  Only a scheduling hint.
-__device__ __forceinline__ int predict_class(int bv, uint64_t ctr, const Args& A, int gi) {
+__device__ __forceinline__ int predict_class(int bv, uint64_t ctr, const Args& A, int gi, uint32_t& cache) {
+    cache = 0u;
     if (rd(bv, R_OVER)) return kClasses - 1;              // next: reset -> opening roll (never doubles)
     Rng r;
-    r.init_philox(ctr, A.key0, A.key1, (uint32_t)gi);
+    const uint64_t c0 = ctr & kCtrMask;
+    r.init_philox(c0, A.key0, A.key1, (uint32_t)gi);
     const int a = r.die(), b = r.die();
+    const uint64_t draws = r.ctr - c0;
+    if (draws < 32) cache = 0x8000u | (uint32_t)a | ((uint32_t)b << 3) | ((uint32_t)draws << 6);
     if (a != b) return kClasses - 1;
     const int nxt = 1 - rd(bv, R_CUR);
     const int l = lane_id();
@@ -233,9 +245,21 @@ __device__ __forceinline__ bool roll_lane(int& bv, int gi, const Args& A, uint32
     const int need = rd(bv, R_NEED);
     if (need == NEED_NONE) return false;
     Rng rng;
-    if (A.dice_mode == BGX_DICE_PHILOX) rng.init_philox(*ctr_io, A.key0, A.key1, (uint32_t)gi);
+    bool cached = false;
+    if (A.dice_mode == BGX_DICE_PHILOX) {
+        const uint32_t cache = (uint32_t)(*ctr_io >> 48);
+        const uint64_t c = *ctr_io & kCtrMask;
+        cached = need != NEED_RESET && (cache & 0x8000u) != 0u;     // the roll predicted last step
+        rng.init_philox(cached ? c + ((cache >> 6) & 31u) : c, A.key0, A.key1, (uint32_t)gi);
+        if (cached) {
+            r0 = (int)(cache & 7u);
+            r1 = (int)((cache >> 3) & 7u);
+            if (lane_id() == 0) A.ctr[gi] = rng.ctr;
+        }
+    }
     else if (A.dice_mode == BGX_DICE_MT_LANE) rng.init_mt(A.mt + (size_t)gi * kMtWords, mt_scratch);
-    if (need == NEED_RESET) {
+    if (cached) {
+    } else if (need == NEED_RESET) {
         if (rd(bv, R_MATCH)) { bv = wr(bv, R_S0, 0); bv = wr(bv, R_S1, 0); bv = wr(bv, R_MATCH, 0); }
         if (lane_id() < 52) bv = initial_byte(lane_id());
         bv = wr(bv, R_OVER, 0);

@@ -45,8 +45,12 @@ __device__ __forceinline__ void step_lane(const Args& A, int gi, uint4* tab, uin
     }
     store_rec(A, gi, bv);
     if (PHASE == 0 && A.cls) {
-        const int c = predict_class(bv, ctr, A, gi);
-        if (lane_id() == 0) A.cls[gi] = (uint8_t)c;
+        uint32_t cache;
+        const int c = predict_class(bv, ctr, A, gi, cache);
+        if (lane_id() == 0) {
+            A.cls[gi] = (uint8_t)c;
+            if (cache) A.ctr[gi] = (ctr & kCtrMask) | ((uint64_t)cache << 48);
+        }
     }
     if (A.stamps && lane_id() == 0) {
         A.stamps[2 * gi] = t0;
@@ -81,8 +85,12 @@ __global__ __launch_bounds__(64) void k_reset(Args A, const uint8_t* lane_mask, 
         bv = advance_lane<LOG>(bv, gi, A, tab, memo, &ctr);
         if (obs) write_obs(bv, obs + (size_t)gi * 198);
         if (A.cls) {
-            const int c = predict_class(bv, ctr, A, gi);
-            if (lane_id() == 0) A.cls[gi] = (uint8_t)c;
+            uint32_t cache;
+            const int c = predict_class(bv, ctr, A, gi, cache);
+            if (lane_id() == 0) {
+                A.cls[gi] = (uint8_t)c;
+                if (cache) A.ctr[gi] = (ctr & kCtrMask) | ((uint64_t)cache << 48);
+            }
         }
     }
     store_rec(A, gi, bv);
