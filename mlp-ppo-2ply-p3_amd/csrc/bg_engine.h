@@ -420,6 +420,7 @@ struct bgx_engine {
     int lds_log;      // 8 .. 11 (the split's doubles prefix; standalone movegen 9 .. 11)
     int memo_mode;    // 0: none, 1: separate memo tables, 2: memo inside the dedup table
     int heavy_wpe;    // 5: the doubles prefix held to 5 waves/SIMD (A/B)
+    int tier1_grid;   // workgroups of the step's first overflow tier
     bool split;       // Philox mode: doubles-prefix launch, then the light launch
     bg::Args a;
     uint4* slow_tables;

@@ -11,6 +11,7 @@
 //   ctr     [B]      u64  per-lane Philox draw counters
 // Kernels are launched one 64-thread workgroup (= one wave) per game.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
@@ -540,8 +541,8 @@ static int heavy_grid(int B, bool xcd) {
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
                      const uint8_t* dice, int cap, int16_t* nm, int32_t* nt, uint64_t* moves) {
     if (src == 0) {
-        hipLaunchKernelGGL((k_movegen_over<0, 1>), dim3(256), dim3(64), 0, s, e->a, boards, players, dice, cap, nm, nt,
-                           moves, e->slow_tables);
+        hipLaunchKernelGGL((k_movegen_over<0, 1>), dim3(e->tier1_grid), dim3(64), 0, s, e->a, boards, players, dice,
+                           cap, nm, nt, moves, e->slow_tables);
         hipLaunchKernelGGL((k_movegen_over<0, 2>), dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice,
                            cap, nm, nt, moves, e->slow_tables);
     } else {
@@ -574,6 +575,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     e->split = !(sp && sp[0] == '0');
     const char* sov = getenv("BGX_STEP_OVERLAP");
     e->step_overlap = sov ? atoi(sov) : 1;
+    const char* t1g = getenv("BGX_TIER1_GRID");      // the step's first overflow tier (A/B)
+    e->tier1_grid = t1g && atoi(t1g) > 0 ? atoi(t1g) : 256;
     const char* mm = getenv("BGX_MEMO_MODE");
     e->memo_mode = mm ? atoi(mm) : 0;
     Args& A = e->a;
@@ -781,7 +784,28 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
         if (A.cls) launch_order(e, s);
     }
     CKL();
-    return slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
+    const int rc = slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
+    if (getenv("BGX_STEP_DEBUG")) {          // overflow-tier queue sizes of this step
+        int32_t q[2] = {0, 0};
+        CK(hipMemcpyAsync(q, A.ovf_count, 8, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        fprintf(stderr, "[bgx step] tier1 %d tier2 %d of %d lanes\n", q[0], q[1], A.B);
+        for (int i = 0; i < q[0] && i < 4; ++i) {
+            int32_t gi = 0;
+            uint8_t rec[64];
+            CK(hipMemcpy(&gi, A.ovf_queue + i, 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(rec, A.lanes + (size_t)gi * 64, 64, hipMemcpyDeviceToHost));
+            int own = 0, outside = 0;
+            const int pl = rec[52];
+            for (int p = 0; p < 24; ++p) {
+                own += rec[pl * 24 + p] > 0;
+                if (!(pl == 0 ? p >= 18 : p < 6)) outside += rec[pl * 24 + p];
+            }
+            fprintf(stderr, "   lane %d pl %d roll %d-%d points %d outside %d bar %d off %d n %d\n", gi, pl, rec[53],
+                    rec[54], own, outside, rec[48 + pl], rec[50 + pl], rec[60] | (rec[61] << 8));
+        }
+    }
+    return rc;
 }
 
 int bgx_movegen(bgx_engine* e, const int8_t* boards52_dev, const uint8_t* players_dev, const uint8_t* dice_dev,
