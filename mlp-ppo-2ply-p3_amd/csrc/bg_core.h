@@ -847,6 +847,19 @@ struct Gen {
         int x2 = -1;
         uint32_t F1 = 0;       // forbidden points below each node (forbid mode)
         if (a1) { const Kids k = gen(t1, d, pl, blocked); q2 = k.bits; c2 = kids(q2, l, d, s0, t1, F1); x2 = k.extra; }
+        if (pure_walk) {
+            // Every state is visited once and no bear-off occurs, so a state's depth is
+            // its length: when some 4-long sequence exists the list is exactly the
+            // 4-long leaves in DFS order (the shorter dead ends are all filtered and
+            // equal none of them) -- one flat pass over every depth-1 node, without
+            // the in-order descent to the first 4-long leaf.  Otherwise (no 4-long
+            // leaf: the dead ends are the list) the walk below runs from the start.
+            flat_depth2(__ballot(a1 && c2 != 0u), t1, c2, x2, (uint64_t)e1, d, F1);
+            if (ovf || cur_max == 4) return;
+            count = 0;
+            cur_max = 0;
+            sink.reset();
+        }
         for (uint32_t b1 = k1.bits; b1; b1 &= b1 - 1u) {
             if (got4) {
                 flat_depth2((uint64_t)b1 & __ballot(c2 != 0u), t1, c2, x2, (uint64_t)e1, d, F1);
