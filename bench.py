@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--host-mirror", action="store_true",
                     help="C3: also copy every rollout row to pinned host memory (PCIe-inclusive rate)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true", help="C2 with eager launches instead of a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
@@ -152,7 +153,7 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 2):
             "losses_last": {k: ms[-1][k] for k in ("policy_loss", "value_loss", "entropy", "total_loss")}}
 
 
-def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 2):
+def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 2, graphs: bool = True):
     """C2: B games per GPU, greedy 1-ply self-play with the value head
     MLP(198->40->1): every step = V over each lane's legal afterstates (mover's
     one-hot, as legal_board_features) -> first argmax -> env.step.  The B games
@@ -181,17 +182,46 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
     for _ in range(20):                                # burn-in + warm
         step()
     torch.cuda.synchronize(dev)
+    # At B = 4,096 a step is a dozen short launches (1-ply pass, split env step,
+    # dispatch order, overflow tiers): replayed as one HIP graph of two steps (the
+    # engine alternates its overflow-counter set every step, so a pair of steps
+    # is a fixed point of its host state).  Every launch reads its state from the
+    # device, so the replays are the same steps as the eager calls.
+    graph = None
+    if S == 1 and graphs:
+        try:
+            cap = torch.cuda.Stream(dev)
+            cap.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(cap):
+                for _ in range(2):
+                    best, _ = one_ply(engs[0], vh)
+                    engs[0].step(best, want_obs=False, want_info=False)
+            torch.cuda.synchronize(dev)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=cap):
+                for _ in range(2):
+                    best, _ = one_ply(engs[0], vh)
+                    engs[0].step(best, want_obs=False, want_info=False)
+            torch.cuda.synchronize(dev)
+        except Exception as ex:                        # eager launches then
+            print(f"[bench] C2 graph capture failed ({ex}); eager", file=sys.stderr)
+            graph = None
     barrier(ws)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    if graph is not None:
+        for _ in range(steps // 2):
+            graph.replay()
+        steps = steps // 2 * 2
+    else:
+        for _ in range(steps):
+            step()
     torch.cuda.synchronize(dev)
     barrier(ws)
     el = max_over_ranks(time.perf_counter() - t0, ws)
     return {"config": f"C2: B={B} games/GPU as {S} shard(s), 1-ply greedy self-play, value MLP 198->40->1 "
                       "(argmax over afterstates)",
             "env_steps_per_s": sum_over_ranks(float(B * steps), ws) / el, "ms_per_step": el * 1e3 / steps,
-            "steps": steps, "shards": S}
+            "steps": steps, "shards": S, "hip_graph": graph is not None}
 
 
 def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
@@ -421,7 +451,8 @@ def main():
         # the same roots with the reference's H = 128 value head (agent/config.py:8)
         line["two_ply_h128"] = two_ply_bench(eng2, 1, ws, dev, hidden=128)
     if args.c2_steps > 0:
-        line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev, args.c2_shards)
+        line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev, args.c2_shards,
+                                                          not args.no_graphs)
     if args.horizon > 0 and args.workload in ("c3", "ppo"):
         line["ppo_iteration"] = ppo_iteration_bench(B, args.horizon, ws, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
