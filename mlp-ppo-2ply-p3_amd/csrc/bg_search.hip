@@ -1178,13 +1178,15 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const float* f16s = vpacked;
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4, value_bias};
-        // BGX_2PLY_LWPE=8: the non-doubles enumerator held to 64 VGPRs (A/B; it spills
-        // and runs slower than at 75 VGPRs / 6 waves per SIMD)
+        // the non-doubles enumerator: the row-level walk held to 80 VGPRs (6 waves/SIMD,
+        // +1.2 % over its natural 91).  A/B: BGX_2PLY_ROWS=0 the per-job walk only;
+        // BGX_2PLY_LWPE=1 the row-level walk without the floor, =8 the per-job walk
+        // held to 64 VGPRs (it spills and runs slower)
         const char* lw = getenv("BGX_2PLY_LWPE");
-        // BGX_2PLY_ROWS=0: the per-job non-doubles walk only (A/B)
         const char* rw = getenv("BGX_2PLY_ROWS");
         void (*klight)(S2) = lw && atoi(lw) == 8 ? k_enum<kLogLight, -1, 0, 8>
-                             : (rw && rw[0] == '0') ? k_enum<kLogLight, -1, 0, 1> : k_enum<kLogLight, -1, 3, 1>;
+                             : (rw && rw[0] == '0') ? k_enum<kLogLight, -1, 0, 1>
+                             : (lw && atoi(lw) == 1) ? k_enum<kLogLight, -1, 3, 1> : k_enum<kLogLight, -1, 3, 6>;
         int g_light = persistent_grid(e, klight, 32);
         int g_heavy = persistent_grid(e, kheavy, 32);
         if (const char* v = getenv("BGX_2PLY_HGRID")) g_heavy = atoi(v) > 0 ? atoi(v) : g_heavy;
