@@ -106,6 +106,12 @@ int bgx_encode(const int8_t* boards52_dev, const uint8_t* players_dev, int32_t n
  * them under autocast).  dtype 0: fp32 [n][198]; 1: fp16 [n][198], the round to
  * nearest of the fp32 features (autocast's cast). */
 int bgx_encode_records(const uint8_t* records_dev, int32_t n, int32_t dtype, void* out_dev, void* stream);
+/* The same with a row width of 198 or 208 elements: columns 198..width-1 are
+ * zero (208: 16-byte aligned rows, which hipBLASLt's vector-load GEMMs need for
+ * the PPO update's fc1 forward and weight gradient; the zero columns meet zero
+ * weight columns, so the products are unchanged). */
+int bgx_encode_records_ex(const uint8_t* records_dev, int32_t n, int32_t dtype, int32_t width, void* out_dev,
+                          void* stream);
 
 /* execute_full_move_on_board_copy (immutable_board.py:224-233) over every legal
  * move of lanes [lane0, lane0+nlanes): boards52 int8[nlanes][max_moves][52]
@@ -231,6 +237,19 @@ int bgx_ppo_head_ex(const void* logits_dev, int32_t dtype, int64_t ld_logits, co
  * in colsum[blocks][hidden] (fp32; the caller sums the rows). */
 int bgx_relu_backward(void* dh, const void* h, int32_t n, int32_t hidden, float* colsum, int32_t blocks,
                       void* stream);
+
+/* The fp16 epoch's fc1 forward from the stored records (ppo_agent.py:274 under
+ * autocast, policy_network.py:69-70): h[n][hidden] fp16 = relu(W1h . fp16(x) + b1h)
+ * with fp32 accumulation, x = the 198 features of each 64-byte record (off/15
+ * rounded to fp16 as autocast's cast rounds it).  W1h [hidden][198] fp16 is packed
+ * once per weight update by bgx_fc1_pack into bgx_fc1_packed_size(hidden) bytes
+ * (16-byte aligned); b1h [hidden] fp16.  hidden % 4 == 0, hidden <= 128; h 8-byte
+ * aligned.  Replaces the materialised feature rows + GEMM for the forward; the
+ * weight gradient still reads the encoded features. */
+int bgx_fc1_packed_size(int32_t hidden);
+int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* stream);
+int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_dev, const void* b1h_dev,
+                    int32_t hidden, void* h_dev, void* stream);
 
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf

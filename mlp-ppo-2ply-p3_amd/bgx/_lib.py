@@ -31,6 +31,7 @@ SIGNATURES = {
     "bgx_movegen": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P]),
     "bgx_encode": (ctypes.c_int, [_P, _P, _I32, _P, _P]),
     "bgx_encode_records": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    "bgx_encode_records_ex": (ctypes.c_int, [_P, _I32, _I32, _I32, _P, _P]),
     "bgx_afterstates": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     "bgx_legal_features": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
     "bgx_action_masks": (ctypes.c_int, [_P, _P, _P, _P]),
@@ -54,6 +55,9 @@ SIGNATURES = {
                                        ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, ctypes.c_int64, _P, _P, _I32,
                                        _P, _P]),
     "bgx_relu_backward": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _I32, _P]),
+    "bgx_fc1_packed_size": (ctypes.c_int, [_I32]),
+    "bgx_fc1_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
+    "bgx_fc1_records": (ctypes.c_int, [_P, _I32, _P, _P, _I32, _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),
 }

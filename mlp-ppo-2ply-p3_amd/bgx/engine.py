@@ -212,19 +212,22 @@ class Engine:
         return nm, nt, mv
 
 
-def encode_records(records: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+def encode_records(records: torch.Tensor, dtype=torch.float32, width: int = 198) -> torch.Tensor:
     """get_board_features of n 64-byte lane records (board bytes 0..51, player to
-    move at 52) as fp32, or fp16 = the fp32 features rounded (autocast's cast)."""
+    move at 52) as fp32, or fp16 = the fp32 features rounded (autocast's cast).
+    width 208: rows padded with 10 zero columns (16-byte aligned GEMM operand)."""
     if records.dim() != 2 or records.shape[1] != 64 or records.element_size() != 1:
         raise ValueError(f"encode_records: records must be [n, 64] bytes, got {tuple(records.shape)} {records.dtype}")
     if dtype not in (torch.float32, torch.float16):
         raise ValueError(f"encode_records: dtype must be float32 or float16, got {dtype}")
+    if width not in (198, 208):
+        raise ValueError(f"encode_records: width must be 198 or 208, got {width}")
     L = _lib.load()
     r = records.contiguous()
-    out = torch.empty(r.shape[0], 198, dtype=dtype, device=r.device)
+    out = torch.empty(r.shape[0], width, dtype=dtype, device=r.device)
     s = ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)
-    check(L.bgx_encode_records(_ptr(r), r.shape[0], 0 if dtype == torch.float32 else 1, _ptr(out), s),
-          "bgx_encode_records")
+    check(L.bgx_encode_records_ex(_ptr(r), r.shape[0], 0 if dtype == torch.float32 else 1, width, _ptr(out), s),
+          "bgx_encode_records_ex")
     return out
 
 

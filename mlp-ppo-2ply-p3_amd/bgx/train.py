@@ -219,6 +219,16 @@ def _wgrad(g: torch.Tensor, x: torch.Tensor, splits: int = 64) -> torch.Tensor:
 # factor min(n, REF_ROWS) / n is applied in fp32 to the summed weight gradients.
 REF_ROWS = 4096
 
+# Feature row width of the manual fp16 epoch: 208 = 198 features + 10 zero columns,
+# so fc1's forward GEMM and weight gradient read 16-byte aligned rows (396-byte rows
+# keep hipBLASLt off its vector-load kernels; tools/gemm_probe_pad.py).  The zero
+# columns meet zero weight columns: every product is unchanged.  BGX_PPO_FEAT_W=198 A/B.
+FEAT_W = int(os.environ.get("BGX_PPO_FEAT_W", "208"))
+# fc1's forward in the manual fp16 epoch runs from the stored records
+# (bgx_fc1_records: 64 B per row instead of the 416-byte feature row + hipBLASLt
+# GEMM); BGX_PPO_FC1=blas keeps the GEMM for A/B.
+FC1_FROM_RECORDS = os.environ.get("BGX_PPO_FC1", "blas") != "blas"
+
 
 def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
     """The fp16-autocast epoch's forward and backward written out (the same
@@ -238,6 +248,8 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
     dev = W1.device
     with torch.no_grad():
         W1h, b1h = W1.half(), b1.half()
+        F_in = W1.shape[1]
+        Kw = None                                   # padded feature width of the chunks, if any
         W2h = torch.zeros(Ap, Hd, dtype=torch.float16, device=dev)
         b2h = torch.zeros(Ap, dtype=torch.float16, device=dev)
         W2h[:A] = Wa.half(); W2h[A] = wv[0].half()
@@ -249,11 +261,24 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
         p = lambda t: ctypes.c_void_p(t.data_ptr())
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         colsum = torch.empty(PPO_COLSUM_BLOCKS, 512, dtype=torch.float32, device=dev)
+        fc1_rec = FC1_FROM_RECORDS and L.bgx_fc1_packed_size(Hd) > 0
+        if fc1_rec:                                 # W1h in the record kernel's fragment order
+            w1pack = torch.empty(L.bgx_fc1_packed_size(Hd), dtype=torch.uint8, device=dev)
+            check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
         hsum = torch.empty(RELU_BLOCKS, Hd, dtype=torch.float32, device=dev)
         for feats, legal, actions, old_logp, returns, adv, records in chunks:
             x = feats.half()
-            # bias + ReLU in the GEMM epilogue (relu commutes with the fp16 rounding)
-            h = torch._addmm_activation(b1h, x, W1h.t())
+            if x.shape[1] != F_in and Kw is None:   # zero-padded rows: zero weight columns to match
+                Kw = x.shape[1]
+                W1h = torch.nn.functional.pad(W1h, (0, Kw - F_in))
+                gW1 = torch.zeros(W1.shape[0], Kw, dtype=torch.float32, device=dev)
+            if fc1_rec:                             # fc1 forward from the 64-byte records (no feature read)
+                h = torch.empty(x.shape[0], Hd, dtype=torch.float16, device=dev)
+                rec = records.contiguous()
+                check(L.bgx_fc1_records(p(rec), rec.shape[0], p(w1pack), p(b1h), Hd, p(h), stream),
+                      "bgx_fc1_records")
+            else:                                   # bias + ReLU in the GEMM epilogue (relu commutes with
+                h = torch._addmm_activation(b1h, x, W1h.t())     # the fp16 rounding)
             y = F.linear(h, W2h, b2h)                      # [m, Ap]: logits | value | 0
             m = y.shape[0]
             vals = y[:, A].contiguous()
@@ -275,7 +300,7 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
         if post != 1.0:
             for t in (gW1, gb1, gW2, gb2):
                 t.mul_(post)
-    W1.grad, b1.grad = gW1, gb1
+    W1.grad, b1.grad = (gW1 if Kw is None else gW1[:, :F_in].contiguous()), gb1
     Wa.grad, ba.grad = gW2[:A].contiguous(), gb2[:A].contiguous()
     wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
 
@@ -401,7 +426,9 @@ class PPOTrainer:
 
         # the fused path's features are encoded once and kept for the 4 epochs
         # (fp16 under autocast: 2^21 rows x 198 x 2 B = 0.8 GB of HBM)
-        feats = [encode_records(recs[s:min(N, s + self.chunk)], torch.float16 if self.amp else torch.float32)
+        manual = self.fused and self.amp and os.environ.get("BGX_PPO_MANUAL", "1") != "0" and _is_policy_mlp(self.net)
+        feats = [encode_records(recs[s:min(N, s + self.chunk)], torch.float16 if self.amp else torch.float32,
+                                width=FEAT_W if manual else 198)
                  for s in range(0, N, self.chunk)] if self.fused else None
 
         def chunks():

@@ -326,9 +326,10 @@ __device__ __forceinline__ void lds_pair(T* o, float a, float b) {
     }
 }
 
-template <typename T>
+template <typename T, int W>
 __global__ __launch_bounds__(256) void k_encode_rec(const uint8_t* __restrict__ records, int n, T* __restrict__ out) {
-    constexpr int kRows = 64, kImg = kRows * 198 * (int)sizeof(T);        // bytes
+    static_assert(W >= 198 && W % 2 == 0 && (W - 198) / 2 <= 13, "row width: 198 features + up to 26 zero columns");
+    constexpr int kRows = 64, kImg = kRows * W * (int)sizeof(T);          // bytes
     __shared__ __attribute__((aligned(16))) uint8_t img[kImg];
     T* im = (T*)img;
     const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(256) void k_encode_rec(const uint8_t* __restrict__ 
         __syncthreads();                                    // the previous image is copied out
         #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            T* o = im + (w + 4 * k) * 198;
+            T* o = im + (w + 4 * k) * W;
             const int v = b[k], v2 = b2[k];
             if (l < 48) {
                 const int P = l >= 24 ? 1 : 0, f = 98 * P + 4 * (l - 24 * P);
@@ -355,11 +356,13 @@ __global__ __launch_bounds__(256) void k_encode_rec(const uint8_t* __restrict__ 
                 lds_pair(o + (l == 48 ? 96 : 194), (float)v * 0.5f, kOff15[v2 & 15]);
             } else if (l == 50) {
                 lds_pair(o + 196, v2 == 0 ? 1.0f : 0.0f, v2 == 0 ? 0.0f : 1.0f);
+            } else if (l < 51 + (W - 198) / 2) {            // zero padding columns (GEMM-aligned rows)
+                lds_pair(o + 198 + 2 * (l - 51), 0.0f, 0.0f);
             }
         }
         __syncthreads();
-        const int nbytes = nr * 198 * (int)sizeof(T);
-        uint8_t* dst = (uint8_t*)(out + (size_t)r0 * 198);
+        const int nbytes = nr * W * (int)sizeof(T);
+        uint8_t* dst = (uint8_t*)(out + (size_t)r0 * W);
         if (((uintptr_t)dst & 15) == 0) {
             for (int q = threadIdx.x; q < nbytes / 16; q += blockDim.x) ((uint4*)dst)[q] = ((const uint4*)img)[q];
             for (int q = (nbytes & ~15) + threadIdx.x; q < nbytes; q += blockDim.x) dst[q] = img[q];
@@ -832,18 +835,29 @@ int bgx_encode(const int8_t* boards52_dev, const uint8_t* players_dev, int32_t n
     return BGX_OK;
 }
 
-int bgx_encode_records(const uint8_t* records_dev, int32_t n, int32_t dtype, void* out_dev, void* stream) {
-    if (n < 0 || (dtype != 0 && dtype != 1) || (n > 0 && (!records_dev || !out_dev))) return BGX_EINVAL;
+int bgx_encode_records_ex(const uint8_t* records_dev, int32_t n, int32_t dtype, int32_t width, void* out_dev,
+                          void* stream) {
+    if (n < 0 || (dtype != 0 && dtype != 1) || (width != 198 && width != 208) || (n > 0 && (!records_dev || !out_dev)))
+        return BGX_EINVAL;
     if (n == 0) return BGX_OK;
     const int blocks = (n + 63) / 64 < 4096 ? (n + 63) / 64 : 4096;
-    if (dtype == 0)
-        hipLaunchKernelGGL(k_encode_rec<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, records_dev, n,
-                           (float*)out_dev);
+    const hipStream_t s = (hipStream_t)stream;
+    if (dtype == 0 && width == 198)
+        hipLaunchKernelGGL((k_encode_rec<float, 198>), dim3(blocks), dim3(256), 0, s, records_dev, n, (float*)out_dev);
+    else if (dtype == 0)
+        hipLaunchKernelGGL((k_encode_rec<float, 208>), dim3(blocks), dim3(256), 0, s, records_dev, n, (float*)out_dev);
+    else if (width == 198)
+        hipLaunchKernelGGL((k_encode_rec<_Float16, 198>), dim3(blocks), dim3(256), 0, s, records_dev, n,
+                           (_Float16*)out_dev);
     else
-        hipLaunchKernelGGL(k_encode_rec<_Float16>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, records_dev, n,
+        hipLaunchKernelGGL((k_encode_rec<_Float16, 208>), dim3(blocks), dim3(256), 0, s, records_dev, n,
                            (_Float16*)out_dev);
     CKL();
     return BGX_OK;
+}
+
+int bgx_encode_records(const uint8_t* records_dev, int32_t n, int32_t dtype, void* out_dev, void* stream) {
+    return bgx_encode_records_ex(records_dev, n, dtype, 198, out_dev, stream);
 }
 
 int bgx_afterstates(bgx_engine* e, int32_t lane0, int32_t nlanes, int8_t* boards52_dev, void* stream) {

@@ -391,6 +391,95 @@ __global__ void k_policy_pack(const float* W1, const float* b1, const float* Wa,
     }
 }
 
+
+// ---- the PPO update's fc1 forward under fp16 autocast, straight from the records
+// (ppo_agent.py:274 autocast + policy_network.py:69-70): h = fp16(relu(W1h . fp16(x)
+// + b1h)) with fp32 accumulation, as the autocast addmm; x = get_board_features of
+// each stored 64-byte record, generated in registers in kperm_src's K order (every
+// feature is the fp16 cast of the fp32 feature: off / 15 rounded as autocast rounds
+// it).  Replaces the [n, 208] fp16 feature read + hipBLASLt GEMM (~270 us per 2^20
+// rows) by a 64-byte record read.  One wave = 32 rows, 4 waves per workgroup; the
+// W1 fragments (13 k-blocks x T tiles x 1 KiB) are read through L1/L2 as in
+// k_policy_act.
+__constant__ static const float kOffDiv15[16] = {
+    0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
+    6.0f / 15.0f, 7.0f / 15.0f, 8.0f / 15.0f, 9.0f / 15.0f, 10.0f / 15.0f, 11.0f / 15.0f,
+    12.0f / 15.0f, 13.0f / 15.0f, 14.0f / 15.0f, 15.0f / 15.0f};
+
+// w1h [hidden][198] fp16 -> fragments [13][T][64] x uint4: lane l of (kb, t) holds
+// W1h[32t + (l & 31)][kperm_src(kb, l >> 5, i)], i = 0..7 (0 where the unit or the
+// feature does not exist)
+__global__ void k_fc1_pack(const _Float16* __restrict__ w1h, int hidden, int T, uint4* __restrict__ out) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= kKB1 * T * 64) return;
+    const int l = g & 63, t = (g >> 6) % T, kb = (g >> 6) / T;
+    const int u = 32 * t + (l & 31);
+    f16x8 v;
+    #pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int src = kperm_src(kb, l >> 5, i);
+        v[i] = (u < hidden && src >= 0) ? w1h[(size_t)u * kIn + src] : (_Float16)0.0f;
+    }
+    out[g] = __builtin_bit_cast(uint4, v);
+}
+
+template <int T>
+__global__ __launch_bounds__(256) void k_fc1_rec(const uint8_t* __restrict__ recs, int n,
+                                                  const uint4* __restrict__ w1f, const _Float16* __restrict__ b1h,
+                                                  int hidden, _Float16* __restrict__ hout) {
+    __shared__ __attribute__((aligned(16))) uint8_t srec[4][32 * 64];
+    const int l = lane_id(), wv = threadIdx.x >> 6;
+    const int row0 = (blockIdx.x * 4 + wv) * 32;
+    if (row0 >= n) return;                              // no block-level sync below
+    {
+        const int r = l >> 1, off = (l & 1) * 32;
+        const int gr = row0 + r < n ? row0 + r : n - 1;
+        const uint4* src = (const uint4*)(recs + (size_t)gr * 64 + off);
+        uint4* dst = (uint4*)(srec[wv] + r * 64 + off);
+        const uint4 v0 = src[0], v1 = src[1];
+        dst[0] = v0;
+        dst[1] = v1;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);                 // lgkmcnt(0): the wave's own LDS stores
+    __builtin_amdgcn_wave_barrier();
+    const int j = l & 31, h = l >> 5;
+    const uint8_t* myrec = srec[wv] + j * 64;
+    f32x16 acc[T];
+    #pragma unroll
+    for (int t = 0; t < T; ++t)
+        #pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int u = 32 * t + hid(r, h);
+            acc[t][r] = u < hidden ? (float)b1h[u] : 0.0f;
+        }
+    #pragma unroll
+    for (int kb = 0; kb < kKB1; ++kb) {
+        f16x8 bf = feats8(myrec, kb, h);
+        if (kb == 12) {                                 // off counts -> fp16(off / 15), as autocast casts x
+            bf[1] = h == 0 ? (_Float16)kOffDiv15[myrec[50] & 15] : (_Float16)0.0f;
+            bf[3] = h == 0 ? (_Float16)kOffDiv15[myrec[51] & 15] : (_Float16)0.0f;
+        }
+        #pragma unroll
+        for (int t = 0; t < T; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(w1f[(kb * T + t) * 64 + l]), bf, acc[t], 0, 0, 0);
+    }
+    if (row0 + j >= n) return;
+    _Float16* orow = hout + (size_t)(row0 + j) * hidden;
+    #pragma unroll
+    for (int t = 0; t < T; ++t)
+        #pragma unroll
+        for (int q = 0; q < 4; ++q) {                   // units 32t + 8q + 4h + 0..3: one 8-byte store
+            const int u = 32 * t + 8 * q + 4 * h;
+            if (u < hidden) {
+                typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                h4 v;
+                #pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = (_Float16)fmaxf(acc[t][4 * q + i], 0.0f);
+                *(h4*)(orow + u) = v;
+            }
+        }
+}
+
 }  // namespace
 
 extern "C" {
@@ -449,6 +538,41 @@ int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed, i
                    float* logits_out, void* stream) {
     return bgx_policy_act_rec(records_dev, n, packed, hidden, n_actions, seed, step, greedy, act_out, logp_out,
                               value_out, logits_out, nullptr, stream);
+}
+
+int bgx_fc1_packed_size(int32_t hidden) {
+    if (hidden <= 0 || hidden > 128 || hidden % 4) return BGX_EINVAL;
+    return kKB1 * ((hidden + 31) / 32) * 64 * 16;
+}
+
+int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* stream) {
+    if (bgx_fc1_packed_size(hidden) < 0 || !w1h_dev || !packed_dev) return BGX_EINVAL;
+    if ((uintptr_t)packed_dev % 16) return BGX_EINVAL;
+    const int T = (hidden + 31) / 32, work = kKB1 * T * 64;
+    hipLaunchKernelGGL(k_fc1_pack, dim3((work + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       (const _Float16*)w1h_dev, hidden, T, (uint4*)packed_dev);
+    return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
+}
+
+int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_dev, const void* b1h_dev,
+                    int32_t hidden, void* h_dev, void* stream) {
+    if (bgx_fc1_packed_size(hidden) < 0 || n < 0 || (n > 0 && (!records_dev || !packed_dev || !b1h_dev || !h_dev)))
+        return BGX_EINVAL;
+    if (((uintptr_t)records_dev | (uintptr_t)packed_dev) % 16 || (uintptr_t)h_dev % 8) return BGX_EINVAL;
+    if (n == 0) return BGX_OK;
+    const int T = (hidden + 31) / 32;
+    const dim3 grid((n + 127) / 128), blk(256);
+    hipStream_t s = (hipStream_t)stream;
+    const uint4* w = (const uint4*)packed_dev;
+    const _Float16* b = (const _Float16*)b1h_dev;
+    _Float16* o = (_Float16*)h_dev;
+    switch (T) {
+        case 1: hipLaunchKernelGGL((k_fc1_rec<1>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
+        case 2: hipLaunchKernelGGL((k_fc1_rec<2>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
+        case 3: hipLaunchKernelGGL((k_fc1_rec<3>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
+        default: hipLaunchKernelGGL((k_fc1_rec<4>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
+    }
+    return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }
 
 }  // extern "C"

@@ -23,6 +23,11 @@ def test_trainer_iteration():
     f32 = encode(flat[:, :52].contiguous(), flat[:, 52].contiguous())
     assert torch.equal(encode_records(flat), f32)
     assert torch.equal(encode_records(flat, torch.float16), f32.half())
+    # 208-wide rows (the update's GEMM operand): the same features, then zeros
+    for dt in (torch.float32, torch.float16):
+        p208 = encode_records(flat, dt, width=208)
+        assert p208.shape == (flat.shape[0], 208)
+        assert torch.equal(p208[:, :198], f32.to(dt)) and not bool(p208[:, 198:].any())
     counts = (recs[..., 60].int() | (recs[..., 61].int() << 8))
     acts = tr.buf["actions"]
     assert bool(((acts < counts) | (counts == 0)).all())
@@ -174,3 +179,39 @@ def test_manual_fp16_epoch_large_batch():
     for name, a, b in zip([n for n, _ in tr.net.named_parameters()], res[False], res[True]):
         rel = ((a - b).norm() / a.norm()).item()
         assert rel < 2e-3, (name, rel)
+
+
+@pytest.mark.parametrize("hidden", [40, 128])
+def test_fc1_from_records_matches_autocast_gemm(hidden):
+    """bgx_fc1_records (fc1 forward of the fp16 epoch from the 64-byte records)
+    == autocast's addmm relu(fp16(x) W1h^T + b1h) on the encoded features: the
+    same fp16 operands and fp32 accumulation, so the outputs agree to the fp16
+    rounding of an fp32 sum taken in another order (<= 1 ulp)."""
+    import ctypes
+    from bgx import _lib
+    from bgx._lib import check
+    from bgx.engine import encode_records
+    from bgx.train import PPOTrainer
+    tr = PPOTrainer(batch=2048, horizon=3, seed=5, hidden=hidden, chunk=8192)
+    tr.rollout()
+    rec = tr.buf["records"].reshape(-1, 64)[:5000].contiguous()        # ragged: not a multiple of 128
+    L = _lib.load()
+    torch.manual_seed(1)
+    W1h = (torch.randn(hidden, 198, device="cuda") * 0.2).half()
+    b1h = (torch.randn(hidden, device="cuda") * 0.1).half()
+    pk = torch.empty(L.bgx_fc1_packed_size(hidden), dtype=torch.uint8, device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    check(L.bgx_fc1_pack(p(W1h), hidden, p(pk), s), "bgx_fc1_pack")
+    h = torch.full((rec.shape[0], hidden), float("nan"), dtype=torch.float16, device="cuda")
+    check(L.bgx_fc1_records(p(rec), rec.shape[0], p(pk), p(b1h), hidden, p(h), s), "bgx_fc1_records")
+    x = encode_records(rec, torch.float16)
+    ref32 = torch.relu(x.float() @ W1h.float().t() + b1h.float())
+    assert torch.isfinite(h).all()
+    ulp = torch.clamp(ref32.abs(), min=2.0 ** -6) * 2.0 ** -10   # floor 1.5e-5: fp32 sum-order noise near 0
+    assert bool(((h.float() - ref32).abs() <= ulp * 1.01).all())
+    blas = torch._addmm_activation(b1h, x, W1h.t())
+    assert bool(((h.float() - blas.float()).abs() <= 2 * ulp).all())
+    assert float((h == blas).float().mean()) > 0.99
+    # bad arguments are refused, not run
+    assert L.bgx_fc1_packed_size(130) < 0 and L.bgx_fc1_packed_size(42) < 0

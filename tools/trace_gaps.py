@@ -1,5 +1,5 @@
 """GPU busy time vs wall time over a kernel trace (rocprofv3 --kernel-trace
-*_kernel_trace.csv): for the window spanning the last `--last` kernels (or
+*_kernel_trace.csv or its *_results.db): for the window spanning the last `--last` kernels (or
 the whole trace) prints the union of kernel intervals, the wall span, and
 the largest idle gaps with the kernels either side of them.
 
@@ -7,6 +7,7 @@ the largest idle gaps with the kernels either side of them.
 """
 import argparse
 import csv
+import sqlite3
 
 
 def main():
@@ -15,8 +16,12 @@ def main():
     ap.add_argument("--after", default=None, help="start the window at the last kernel whose name holds this")
     ap.add_argument("--top", type=int, default=12)
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
-    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    if a.trace.endswith(".db"):                     # rocprofv3's default SQLite output
+        con = sqlite3.connect(a.trace)
+        ks = sorted((int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels"))
+    else:
+        rows = list(csv.DictReader(open(a.trace)))
+        ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     if a.after:
         idx = [i for i, k in enumerate(ks) if a.after in k[2]]
         ks = ks[idx[-1]:] if idx else ks
