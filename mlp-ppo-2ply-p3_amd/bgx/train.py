@@ -227,7 +227,7 @@ FEAT_W = int(os.environ.get("BGX_PPO_FEAT_W", "208"))
 # fc1's forward in the manual fp16 epoch runs from the stored records
 # (bgx_fc1_records: 64 B per row instead of the 416-byte feature row + hipBLASLt
 # GEMM); BGX_PPO_FC1=blas keeps the GEMM for A/B.
-FC1_FROM_RECORDS = os.environ.get("BGX_PPO_FC1", "blas") != "blas"
+FC1_FROM_RECORDS = os.environ.get("BGX_PPO_FC1", "records") != "blas"
 
 
 def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):

@@ -398,9 +398,8 @@ __global__ void k_policy_pack(const float* W1, const float* b1, const float* Wa,
 // each stored 64-byte record, generated in registers in kperm_src's K order (every
 // feature is the fp16 cast of the fp32 feature: off / 15 rounded as autocast rounds
 // it).  Replaces the [n, 208] fp16 feature read + hipBLASLt GEMM (~270 us per 2^20
-// rows) by a 64-byte record read.  One wave = 32 rows, 4 waves per workgroup; the
-// W1 fragments (13 k-blocks x T tiles x 1 KiB) are read through L1/L2 as in
-// k_policy_act.
+// rows) by a 64-byte record read.  One wave = 32 rows per pass, 4 waves per
+// workgroup sharing the W1 fragments (13 k-blocks x T tiles x 1 KiB) in LDS.
 __constant__ static const float kOffDiv15[16] = {
     0.0f / 15.0f, 1.0f / 15.0f, 2.0f / 15.0f, 3.0f / 15.0f, 4.0f / 15.0f, 5.0f / 15.0f,
     6.0f / 15.0f, 7.0f / 15.0f, 8.0f / 15.0f, 9.0f / 15.0f, 10.0f / 15.0f, 11.0f / 15.0f,
@@ -427,57 +426,81 @@ template <int T>
 __global__ __launch_bounds__(256) void k_fc1_rec(const uint8_t* __restrict__ recs, int n,
                                                   const uint4* __restrict__ w1f, const _Float16* __restrict__ b1h,
                                                   int hidden, _Float16* __restrict__ hout) {
+    // the W1 fragments live in LDS for the workgroup's lifetime (T = 4: 52 KiB); each
+    // wave walks 32-row tiles grid-strided, the next tile's records loaded behind the
+    // current tile's MFMAs (read per wave from L2 they were 52 KiB per 32 rows: the
+    // kernel ran at the L2's rate, 195 us per 2^20 rows)
+    __shared__ uint4 sw[kKB1 * T * 64];
     __shared__ __attribute__((aligned(16))) uint8_t srec[4][32 * 64];
+    for (int i = threadIdx.x; i < kKB1 * T * 64; i += blockDim.x) sw[i] = w1f[i];
+    __syncthreads();
     const int l = lane_id(), wv = threadIdx.x >> 6;
-    const int row0 = (blockIdx.x * 4 + wv) * 32;
-    if (row0 >= n) return;                              // no block-level sync below
-    {
-        const int r = l >> 1, off = (l & 1) * 32;
-        const int gr = row0 + r < n ? row0 + r : n - 1;
+    const int j = l & 31, h = l >> 5;
+    const int ntiles = (n + 31) / 32, stride = gridDim.x * 4;
+    int tile = blockIdx.x * 4 + wv;
+    const int r = l >> 1, off = (l & 1) * 32;
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+    if (tile < ntiles) {
+        const int gr = tile * 32 + r < n ? tile * 32 + r : n - 1;
         const uint4* src = (const uint4*)(recs + (size_t)gr * 64 + off);
+        v0 = src[0];
+        v1 = src[1];
+    }
+    float bias[T][16];
+    #pragma unroll
+    for (int t = 0; t < T; ++t)
+        #pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int u = 32 * t + hid(q, h);
+            bias[t][q] = u < hidden ? (float)b1h[u] : 0.0f;
+        }
+    for (; tile < ntiles; tile += stride) {
+        const int row0 = tile * 32;
         uint4* dst = (uint4*)(srec[wv] + r * 64 + off);
-        const uint4 v0 = src[0], v1 = src[1];
         dst[0] = v0;
         dst[1] = v1;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);                 // lgkmcnt(0): the wave's own LDS stores
-    __builtin_amdgcn_wave_barrier();
-    const int j = l & 31, h = l >> 5;
-    const uint8_t* myrec = srec[wv] + j * 64;
-    f32x16 acc[T];
-    #pragma unroll
-    for (int t = 0; t < T; ++t)
-        #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int u = 32 * t + hid(r, h);
-            acc[t][r] = u < hidden ? (float)b1h[u] : 0.0f;
+        __builtin_amdgcn_wave_barrier();
+        if (tile + stride < ntiles) {                   // next tile's records in flight
+            const int nr = (tile + stride) * 32 + r;
+            const uint4* src = (const uint4*)(recs + (size_t)(nr < n ? nr : n - 1) * 64 + off);
+            v0 = src[0];
+            v1 = src[1];
         }
-    #pragma unroll
-    for (int kb = 0; kb < kKB1; ++kb) {
-        f16x8 bf = feats8(myrec, kb, h);
-        if (kb == 12) {                                 // off counts -> fp16(off / 15), as autocast casts x
-            bf[1] = h == 0 ? (_Float16)kOffDiv15[myrec[50] & 15] : (_Float16)0.0f;
-            bf[3] = h == 0 ? (_Float16)kOffDiv15[myrec[51] & 15] : (_Float16)0.0f;
-        }
+        const uint8_t* myrec = srec[wv] + j * 64;
+        f32x16 acc[T];
         #pragma unroll
         for (int t = 0; t < T; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(w1f[(kb * T + t) * 64 + l]), bf, acc[t], 0, 0, 0);
-    }
-    if (row0 + j >= n) return;
-    _Float16* orow = hout + (size_t)(row0 + j) * hidden;
-    #pragma unroll
-    for (int t = 0; t < T; ++t)
+            #pragma unroll
+            for (int q = 0; q < 16; ++q) acc[t][q] = bias[t][q];
         #pragma unroll
-        for (int q = 0; q < 4; ++q) {                   // units 32t + 8q + 4h + 0..3: one 8-byte store
-            const int u = 32 * t + 8 * q + 4 * h;
-            if (u < hidden) {
-                typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-                h4 v;
-                #pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = (_Float16)fmaxf(acc[t][4 * q + i], 0.0f);
-                *(h4*)(orow + u) = v;
+        for (int kb = 0; kb < kKB1; ++kb) {
+            f16x8 bf = feats8(myrec, kb, h);
+            if (kb == 12) {                             // off counts -> fp16(off / 15), as autocast casts x
+                bf[1] = h == 0 ? (_Float16)kOffDiv15[myrec[50] & 15] : (_Float16)0.0f;
+                bf[3] = h == 0 ? (_Float16)kOffDiv15[myrec[51] & 15] : (_Float16)0.0f;
             }
+            #pragma unroll
+            for (int t = 0; t < T; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(sw[(kb * T + t) * 64 + l]), bf, acc[t], 0, 0, 0);
         }
+        __builtin_amdgcn_wave_barrier();                // srec reads done before the next tile's stores
+        if (row0 + j < n) {
+            _Float16* orow = hout + (size_t)(row0 + j) * hidden;
+            #pragma unroll
+            for (int t = 0; t < T; ++t)
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) {           // units 32t + 8q + 4h + 0..3: one 8-byte store
+                    const int u = 32 * t + 8 * q + 4 * h;
+                    if (u < hidden) {
+                        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                        h4 v;
+                        #pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] = (_Float16)fmaxf(acc[t][4 * q + i], 0.0f);
+                        *(h4*)(orow + u) = v;
+                    }
+                }
+        }
+    }
 }
 
 }  // namespace
@@ -561,7 +584,8 @@ int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_de
     if (((uintptr_t)records_dev | (uintptr_t)packed_dev) % 16 || (uintptr_t)h_dev % 8) return BGX_EINVAL;
     if (n == 0) return BGX_OK;
     const int T = (hidden + 31) / 32;
-    const dim3 grid((n + 127) / 128), blk(256);
+    const int tiles4 = (n + 127) / 128;                 // 4 waves x 32 rows per workgroup and pass
+    const dim3 grid(tiles4 < 1024 ? tiles4 : 1024), blk(256);
     hipStream_t s = (hipStream_t)stream;
     const uint4* w = (const uint4*)packed_dev;
     const _Float16* b = (const _Float16*)b1h_dev;
