@@ -131,7 +131,7 @@ def cpu_baseline(seconds: float):
     return out
 
 
-def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 2):
+def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4):
     """Full PPO iterations (rollout of `horizon` steps on B lanes + 4-epoch update
     with the gradient all-reduce across ranks): env steps/s INCLUDING the update."""
     from bgx.train import PPOTrainer
