@@ -154,7 +154,7 @@ class _PPOHead(torch.autograd.Function):
 
 
 def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_coef: float, group=None,
-              amp: bool = True, fused: bool | None = None, step: bool = True):
+              amp: bool = True, fused: bool | None = None, step: bool = True, sync: bool = True):
     """One full-batch PPO epoch (ppo_agent.py:268-305) over `chunks` =
     iterable of (features, legal_mask, actions, old_logp, returns, advantages
     [, records]), with gradient accumulation and one all-reduce.  Returns loss
@@ -168,7 +168,7 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
     if fused is None:
         fused = dev_type == "cuda"
     if fused:
-        return _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step)
+        return _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync)
     for feats, legal, actions, old_logp, returns, adv, *_ in chunks:
         w = feats.shape[0] / n_total
         with autocast(device_type=dev_type, enabled=amp):
@@ -305,7 +305,7 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
     wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
 
 
-def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step):
+def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync=True):
     dev = next(net.parameters()).device
     if scaler.is_enabled():
         scaler.scale(torch.ones((), device=dev))          # initialises the scale tensor lazily
@@ -329,6 +329,9 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
         allreduce_mean_([p.grad for p in net.parameters() if p.grad is not None], group)
         scaler.step(optimizer)
         scaler.update()
+    if not sync:        # loss parts stay on the device (fp64, same arithmetic): no host sync per epoch
+        m = sums / n_total
+        return torch.cat([m, (m[0] + VALUE_LOSS_COEF * m[1] - entropy_coef * m[2]).reshape(1)])
     pol, val, ent = (sums / n_total).tolist()
     tot = pol + VALUE_LOSS_COEF * val - entropy_coef * ent
     return torch.tensor([pol, val, ent, tot], dtype=torch.float64)
@@ -444,10 +447,11 @@ class PPOTrainer:
                     f, legal = features_and_masks(recs[s:e], self.A)
                 yield f, legal, acts[s:e], old[s:e], R[s:e], adv[s:e], recs[s:e]
 
-        parts = torch.zeros(4, dtype=torch.float64)
+        parts = None
         for _ in range(NUM_EPOCHS):
-            parts += ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
-                               amp=self.amp, fused=self.fused)
+            e = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
+                          amp=self.amp, fused=self.fused, sync=False)
+            parts = e if parts is None else parts + e
         progress = min(1.0, self.total_episodes / ENTROPY_ANNEAL_EPISODES)       # ppo_agent.py:193-197
         self.entropy_coef = ENTROPY_COEF_START - progress * (ENTROPY_COEF_START - ENTROPY_COEF_END)
         p = (parts / NUM_EPOCHS).tolist()
