@@ -423,21 +423,24 @@ __global__ void k_fc1_pack(const _Float16* __restrict__ w1h, int hidden, int T, 
 }
 
 template <int T>
-__global__ __launch_bounds__(256) void k_fc1_rec(const uint8_t* __restrict__ recs, int n,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_fc1_rec(const uint8_t* __restrict__ recs, int n,
                                                   const uint4* __restrict__ w1f, const _Float16* __restrict__ b1h,
                                                   int hidden, _Float16* __restrict__ hout) {
-    // the W1 fragments live in LDS for the workgroup's lifetime (T = 4: 52 KiB); each
-    // wave walks 32-row tiles grid-strided, the next tile's records loaded behind the
+    // the W1 fragments live in LDS for the workgroup's lifetime (T = 4: 52 KiB, shared by
+    // 8 waves; the bias is added in the epilogue from LDS, as the GEMM epilogue adds it, so
+    // the kernel fits 128 VGPRs: 4 waves/SIMD); each wave walks 32-row tiles grid-strided, the next tile's records loaded behind the
     // current tile's MFMAs (read per wave from L2 they were 52 KiB per 32 rows: the
     // kernel ran at the L2's rate, 195 us per 2^20 rows)
     __shared__ uint4 sw[kKB1 * T * 64];
-    __shared__ __attribute__((aligned(16))) uint8_t srec[4][32 * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t srec[8][32 * 64];
+    __shared__ float sb[32 * T];
     for (int i = threadIdx.x; i < kKB1 * T * 64; i += blockDim.x) sw[i] = w1f[i];
+    for (int i = threadIdx.x; i < 32 * T; i += blockDim.x) sb[i] = i < hidden ? (float)b1h[i] : 0.0f;
     __syncthreads();
     const int l = lane_id(), wv = threadIdx.x >> 6;
     const int j = l & 31, h = l >> 5;
-    const int ntiles = (n + 31) / 32, stride = gridDim.x * 4;
-    int tile = blockIdx.x * 4 + wv;
+    const int ntiles = (n + 31) / 32, stride = gridDim.x * 8;
+    int tile = blockIdx.x * 8 + wv;
     const int r = l >> 1, off = (l & 1) * 32;
     uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
     if (tile < ntiles) {
@@ -446,14 +449,6 @@ __global__ __launch_bounds__(256) void k_fc1_rec(const uint8_t* __restrict__ rec
         v0 = src[0];
         v1 = src[1];
     }
-    float bias[T][16];
-    #pragma unroll
-    for (int t = 0; t < T; ++t)
-        #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int u = 32 * t + hid(q, h);
-            bias[t][q] = u < hidden ? (float)b1h[u] : 0.0f;
-        }
     for (; tile < ntiles; tile += stride) {
         const int row0 = tile * 32;
         uint4* dst = (uint4*)(srec[wv] + r * 64 + off);
@@ -471,7 +466,7 @@ __global__ __launch_bounds__(256) void k_fc1_rec(const uint8_t* __restrict__ rec
         #pragma unroll
         for (int t = 0; t < T; ++t)
             #pragma unroll
-            for (int q = 0; q < 16; ++q) acc[t][q] = bias[t][q];
+            for (int q = 0; q < 16; ++q) acc[t][q] = 0.0f;
         #pragma unroll
         for (int kb = 0; kb < kKB1; ++kb) {
             f16x8 bf = feats8(myrec, kb, h);
@@ -495,7 +490,7 @@ __global__ __launch_bounds__(256) void k_fc1_rec(const uint8_t* __restrict__ rec
                         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
                         h4 v;
                         #pragma unroll
-                        for (int i = 0; i < 4; ++i) v[i] = (_Float16)fmaxf(acc[t][4 * q + i], 0.0f);
+                        for (int i = 0; i < 4; ++i) v[i] = (_Float16)fmaxf(acc[t][4 * q + i] + sb[u + i], 0.0f);
                         *(h4*)(orow + u) = v;
                     }
                 }
@@ -584,8 +579,8 @@ int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_de
     if (((uintptr_t)records_dev | (uintptr_t)packed_dev) % 16 || (uintptr_t)h_dev % 8) return BGX_EINVAL;
     if (n == 0) return BGX_OK;
     const int T = (hidden + 31) / 32;
-    const int tiles4 = (n + 127) / 128;                 // 4 waves x 32 rows per workgroup and pass
-    const dim3 grid(tiles4 < 1024 ? tiles4 : 1024), blk(256);
+    const int tiles8 = (n + 255) / 256;                 // 8 waves x 32 rows per workgroup and pass
+    const dim3 grid(tiles8 < 512 ? tiles8 : 512), blk(512);
     hipStream_t s = (hipStream_t)stream;
     const uint4* w = (const uint4*)packed_dev;
     const _Float16* b = (const _Float16*)b1h_dev;
