@@ -3,19 +3,30 @@
 Default workload (N=1 line): BASELINE config C3 — B=65,536 concurrent games per
 GPU, one PPO rollout step per iteration = policy forward (BackgammonPolicyNetwork
 198->128->{500 logits, 1 value}) + masked-softmax sampling + env.step on every
-lane + rollout record (int8 lane boards, action, log-prob, value, reward, done)
-copied to pinned host memory.  `value` = env steps/s summed over ranks.
+lane + rollout row (int8 lane boards, action, log-prob, value, reward, done)
+stored to a device ring in HBM.  The `host_mirror` sub-object times the same
+step with every row also copied to pinned host memory (PCIe-inclusive, the
+reference's host-side rollout, ppo_agent.py:175-187).  `value` = env steps/s
+summed over ranks.
 
-  python bench.py --gpus N --steps K --warmup W [--workload c3|c1|c4]
+  python bench.py --gpus N --steps K --warmup W [--workload c3|c1]
 
-Multi-GPU: one process per GPU (torchrun), independent game shards (weak
-scaling), no collective on the rollout path; barrier + max-over-ranks timing.
+Multi-GPU: one process per GPU, independent game shards (weak scaling), no
+collective on the rollout path; barrier + max-over-ranks timing.  Launched as
+`torch.distributed.run ... bench.py --gpus N` (the driver) each rank reads
+RANK / LOCAL_RANK / WORLD_SIZE; `python bench.py --gpus N` with no WORLD_SIZE
+in the environment starts the N ranks itself (torch.distributed.run as a child
+process; this parent never touches the GPU) and exits with their status.
+Backend "nccl" (= RCCL over xGMI); BGX_DIST_BACKEND=gloo lets several ranks
+share one GPU for rehearsals.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -51,28 +62,67 @@ def parse():
                     help="untimed steps before warmup so the game population reaches its steady mix "
                          "(openings are cheaper than mid-game positions)")
     ap.add_argument("--host-mirror", action="store_true",
-                    help="C3: also copy every rollout row to pinned host memory (PCIe-inclusive rate)")
+                    help="C3 headline with every rollout row also copied to pinned host memory (PCIe-inclusive)")
+    ap.add_argument("--mirror-steps", type=int, default=64,
+                    help="steps of the host_mirror sub-object (C3 + pinned-host copy of every row; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graphs", action="store_true", help="C2 with eager launches instead of a HIP graph")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
 
-def dist_init():
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: run this same command as N
+    ranks under torch.distributed.run (one process per GPU) in a child process
+    and return its exit status.  Called before anything touches the GPU; the
+    ranks' stdout is this process's stdout, so rank 0's JSON line is the output."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC only on this driver (RCCL)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dist_init(gpus: int):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
+    if ws != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}")
+    ndev = torch.cuda.device_count()
+    backend = os.environ.get("BGX_DIST_BACKEND", "nccl")
+    if ws > 1 and backend == "nccl" and ws > ndev:
+        raise SystemExit(f"bench.py: {ws} RCCL ranks need {ws} GPUs, {ndev} visible "
+                         "(BGX_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(ndev, 1)
     torch.cuda.set_device(local)
     if ws > 1:
         import torch.distributed as dist
         # "nccl" is RCCL on ROCm (one rank per GPU); BGX_DIST_BACKEND=gloo lets
         # several ranks share one GPU for functional rehearsals of the N>1 path
-        backend = os.environ.get("BGX_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    return rank, ws, local
+    return rank, ws, local, backend if ws > 1 else None
+
+
+def gather_ranks(x, ws: int) -> list:
+    """Every rank's list of floats, in rank order (a CUDA tensor: RCCL and gloo)."""
+    t = torch.tensor(x, dtype=torch.float64, device="cuda")
+    if ws == 1:
+        return [x]
+    import torch.distributed as dist
+    out = [torch.empty_like(t) for _ in range(ws)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
 
 
 def barrier(ws):
@@ -146,11 +196,21 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4):
     barrier(ws)
     el = max_over_ranks(time.perf_counter() - t0, ws)
     steps = sum_over_ranks(float(B * horizon * iters), ws)
-    return {"config": f"PPO iteration: B={B}/GPU x T={horizon} rollout + 4-epoch full-batch update "
-                      f"(chunked, features re-encoded from int8 records), grad all-reduce over {ws} rank(s)",
-            "env_steps_per_s_incl_update": steps / el, "seconds_per_iteration": el / iters,
-            "rollout_s": sum(m["rollout_s"] for m in ms) / iters, "update_s": sum(m["update_s"] for m in ms) / iters,
-            "losses_last": {k: ms[-1][k] for k in ("policy_loss", "value_loss", "entropy", "total_loss")}}
+    out = {"config": f"PPO iteration: B={B}/GPU x T={horizon} rollout + 4-epoch full-batch update "
+                     f"(chunked, features re-encoded from int8 records), grad all-reduce over {ws} rank(s)",
+           "ranks": ws, "env_steps_per_s_incl_update": steps / el, "seconds_per_iteration": el / iters,
+           "rollout_s": sum(m["rollout_s"] for m in ms) / iters, "update_s": sum(m["update_s"] for m in ms) / iters,
+           "losses_last": {k: ms[-1][k] for k in ("policy_loss", "value_loss", "entropy", "total_loss")}}
+    if ws > 1:      # data parallel: the all-reduced update leaves every rank on the same weights
+        import torch.distributed as dist
+        flat = torch.cat([p.detach().reshape(-1) for p in tr.net.parameters()])
+        allw = [torch.empty_like(flat) for _ in range(ws)]
+        dist.all_gather(allw, flat)
+        out["weights_identical_across_ranks"] = all(torch.equal(allw[0], w) for w in allw)
+        out["collective"] = ("one flat fp32 gradient all-reduce per optimizer step (4 per update) + the "
+                             "(sum r, sum r^2, n) return-normalisation all-reduce, backend "
+                             + dist.get_backend())
+    return out
 
 
 def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 2, graphs: bool = True):
@@ -272,9 +332,35 @@ def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
                                  "as a feature)"}}
 
 
+def issue_roofline(sq: dict, lanes: int, kern_ms: float, src) -> dict:
+    """The env step's real bound: instruction issue, not HBM.  Wave-instructions per
+    lane-step by pipe (SQ_INSTS_* of the C3 step alone, profiles/latest_summary.json,
+    tools/profile.sh passes sqi/sqc) x the lanes of one shard step, over the live
+    HIP-event time of that step, against each pipe's chip capacity (VALU: 2 cycles per
+    wave64 instruction on each of 1,024 SIMD-32s; SALU, LDS, SMEM, VMEM, branch: one
+    instruction per cycle on each of 256 CUs; 2.4 GHz).  frac = the busiest pipe's
+    utilisation.  The wave-time split says where the rest of each wave's time goes."""
+    ins, model, ghz = sq["instructions_per_lane_step"], sq["pipe_model"], sq["clock_ghz"]
+    t = kern_ms * 1e-3
+    pipes = {}
+    for p, m in model.items():
+        n = ins.get(m["counter"], 0.0) * lanes
+        pipes[p] = {"wave_insts_per_lane_step": ins.get(m["counter"], 0.0),
+                    "achieved_G_per_s": n / t / 1e9, "peak_G_per_s": m["units"] * ghz / m["cycles_per_inst"],
+                    "frac": n * m["cycles_per_inst"] / m["units"] / (ghz * 1e9) / t}
+    top = max(pipes, key=lambda p: pipes[p]["frac"])
+    return {"kernel": "env step (same launches and HIP-event window as `roofline`)", "bound": "issue",
+            "pipe": top, "achieved": pipes[top]["achieved_G_per_s"], "peak": pipes[top]["peak_G_per_s"],
+            "unit": "G wave-instructions/s", "frac": pipes[top]["frac"], "pipes": pipes,
+            "wave_time_split": sq.get("wave_time_split"), "lanes_per_launch": lanes, "kernel_ms": kern_ms,
+            "counters_source": src}
+
+
 def main():
     args = parse()
-    rank, ws, local = dist_init()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    rank, ws, local, backend = dist_init(args.gpus)
     dev = torch.device("cuda", local)
     import bgx
     from bgx.policy import PolicyNet
@@ -308,13 +394,14 @@ def main():
         "reward": torch.empty(ring, Bs, dtype=torch.float32, **kw),
         "done": torch.empty(ring, Bs, dtype=torch.uint8, **kw),
     } for _ in range(S)]
+    want_mirror = args.host_mirror or args.mirror_steps > 0
     pins = [{k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in b.items()}
-            for b in bufs] if args.host_mirror else None
-    copy_streams = [torch.cuda.Stream(dev) for _ in range(S)] if args.host_mirror else None
+            for b in bufs] if want_mirror else None
+    copy_streams = [torch.cuda.Stream(dev) for _ in range(S)] if want_mirror else None
     counts = [torch.empty(Bs, dtype=torch.int16, device=dev) for _ in range(S)]
     gen = torch.Generator(device=dev).manual_seed(99 + rank)
     ev_pairs = []
-    state = {"i": 0}
+    state = {"i": 0, "mirror": args.host_mirror}
 
     def shard_step(k, i, timed):
         e, st = engs[k], streams[k]
@@ -342,7 +429,7 @@ def main():
             if timed:
                 e1.record(st)
                 ev_pairs.append((e0, e1))
-            if pins is not None:                                  # optional pinned-host mirror (side stream)
+            if state["mirror"]:                                   # pinned-host mirror (side stream)
                 cs = copy_streams[k]
                 cs.wait_stream(st)
                 with torch.cuda.stream(cs):
@@ -380,8 +467,10 @@ def main():
     torch.cuda.synchronize(dev)
     barrier(ws)
     torch.cuda.synchronize(dev)
-    el = max_over_ranks(time.perf_counter() - t0, ws)
-    total_steps = sum_over_ranks(float(B * args.steps), ws)
+    el_rank = time.perf_counter() - t0
+    el = max_over_ranks(el_rank, ws)
+    per_rank = gather_ranks([float(B * args.steps), el_rank], ws)
+    total_steps = sum(r[0] for r in per_rank)
     value = total_steps / el
     kern_ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
     # algorithmic bytes per lane-step of the env-step kernel:
@@ -393,7 +482,7 @@ def main():
     # passes (tools/profile.sh -> profiles/latest_summary.json; (FETCH_SIZE + WRITE_SIZE)
     # x 1024: the step's 64-B record / 4-8-B scalar reads are single 64-B requests that
     # FETCH_SIZE counts exactly, calibrated in profiles/r2_fetch_calibration.json)
-    traffic, traffic_src, prof_kernels = None, None, None
+    traffic, traffic_src, prof_kernels, sq = None, None, None, None
     prof = os.path.join(ROOT, "profiles", "latest_summary.json")
     if os.path.exists(prof):
         try:
@@ -402,6 +491,7 @@ def main():
             if env and env["hbm_bytes_per_step"] > 0:
                 traffic, traffic_src = env["hbm_bytes_per_step"], summ.get("command")
                 prof_kernels = {k["name"]: round(k["avg_ns"] / 1e3, 1) for k in env["kernels"]}
+            sq = (env or {}).get("sq")
         except Exception:
             traffic = None
     line = {
@@ -426,8 +516,9 @@ def main():
                    "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
                    "parallelism": f"dp{ws} (independent game shards)", "shards_per_gpu": S,
                    "streams_per_gpu": S},
-        "roofline": {"kernel": "env step = k_step<0,10,1> (predicted-doubles prefix) then k_step<0,8,0,true> "
-                               "(the rest) + k_order_count/scatter + k_movegen_over tiers, one wave per game, "
+        "roofline": {"kernel": "env step = k_step<0,9,0,false,1> (predicted-doubles prefix) then "
+                               "k_step<0,8,0,true,1> (the rest) + k_order_count/scatter + k_movegen_over tiers, "
+                               "one wave per game, "
                                "the light launch on the engine's side stream (event fork-join); HIP events around "
                                "bgx_step on the shard's stream, per shard of games_per_gpu/shards lanes",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -439,6 +530,34 @@ def main():
                      "rocprof_avg_us": prof_kernels,
                      "mean_legal_moves": mean_moves},
     }
+    line["per_rank"] = [{"rank": k, "env_steps": r[0], "seconds": r[1]} for k, r in enumerate(per_rank)]
+    if ws > 1:
+        line["dist_backend"] = backend
+    if args.mirror_steps > 0 and not args.host_mirror and args.workload == "c3":
+        # north_star's "rollout into pinned host buffers": the same C3 step with every
+        # rollout row also copied to pinned host memory on a side stream (PCIe-inclusive)
+        state["mirror"] = True
+        for _ in range(2):
+            step(False)
+        torch.cuda.synchronize(dev)
+        barrier(ws)
+        t0 = time.perf_counter()
+        for _ in range(args.mirror_steps):
+            step(False)
+        for cs in copy_streams:
+            torch.cuda.current_stream(dev).wait_stream(cs)
+        torch.cuda.synchronize(dev)
+        barrier(ws)
+        elm = max_over_ranks(time.perf_counter() - t0, ws)
+        state["mirror"] = False
+        line["host_mirror"] = {
+            "config": "C3 as the headline + every rollout row (64-B record, action, log-prob, value, reward, "
+                      "done: 81 B per lane-step) copied to pinned host memory on a side stream per shard",
+            "env_steps_per_s": sum_over_ranks(float(B * args.mirror_steps), ws) / elm,
+            "ms_per_step": elm * 1e3 / args.mirror_steps, "steps": args.mirror_steps,
+            "host_bytes_per_step_per_gpu": B * 81}
+    if sq and sq.get("instructions_per_lane_step") and args.workload == "c3":
+        line["roofline_issue"] = issue_roofline(sq, Bs, kern_ms, summ.get("pmc_command"))
     if args.two_ply_batches > 0:
         eng2 = engs[0] if S == 1 else bgx.Engine(batch=B, max_moves=500, seed=77 + rank, dice="philox",
                                                  auto_reset=True, device=dev)

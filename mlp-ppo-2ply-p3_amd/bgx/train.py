@@ -14,6 +14,16 @@ GradScaler + Adam, clip 0.25, 0.5*MSE, -c_ent*H) but computed in chunks with
 gradient accumulation (features re-encoded from the stored records by the HIP
 encoder) and ONE all-reduce of the gradients per epoch across ranks.
 
+Entropy coefficient (`entropy_anneal`): the reference's update always calls
+update_entropy_coef (ppo_agent.py:193-197), which anneals by
+`agent.total_episodes`.  Its vectorised driver train.py never increments that
+counter (it counts a module-global `total_episodes`, train.py:74), so under
+train.py the coefficient stays at ENTROPY_COEF_START = 0.15 for the whole run;
+train_single.py increments `agent.total_episodes` per episode (train_single.py:78)
+and the coefficient anneals to 0.01 over 400,000 episodes.  PPOTrainer restates
+train.py, so `entropy_anneal="train"` (constant 0.15) is the default;
+`"train_single"` anneals by the episodes finished in the rollouts.
+
 Returns: `returns="lane"` (default) discounts within each game lane;
 `returns="reference"` reproduces the reference's quirk of discounting over the
 flat step-major memory in which the environments are interleaved
@@ -106,6 +116,16 @@ def reference_returns(rewards: torch.Tensor, dones: torch.Tensor, gamma: float =
         R = flat_r[k] + gamma * R
         out[k] = R
     return torch.tensor(out, dtype=torch.float32, device=rewards.device).view_as(rewards)
+
+
+def entropy_coef_after_update(mode: str, total_episodes: int) -> float:
+    """update_entropy_coef (ppo_agent.py:193-197) as each reference driver feeds it:
+    train.py leaves agent.total_episodes at 0 (it increments a module global,
+    train.py:74), so the coefficient stays at the start value; train_single.py
+    counts every episode into it (train_single.py:78)."""
+    episodes = total_episodes if mode == "train_single" else 0
+    progress = min(1.0, episodes / ENTROPY_ANNEAL_EPISODES)
+    return ENTROPY_COEF_START - progress * (ENTROPY_COEF_START - ENTROPY_COEF_END)
 
 
 def features_and_masks(records: torch.Tensor, n_actions: int):
@@ -340,7 +360,11 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
 class PPOTrainer:
     def __init__(self, batch: int = 65536, horizon: int = 64, hidden: int = 128, n_actions: int = 500,
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
-                 chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True):
+                 chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True,
+                 entropy_anneal: str = "train"):
+        if entropy_anneal not in ("train", "train_single"):
+            raise ValueError(f"entropy_anneal must be 'train' or 'train_single', got {entropy_anneal!r}")
+        self.entropy_anneal = entropy_anneal
         self.dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.group = process_group
         self.rank = dist.get_rank(process_group) if _world(process_group) > 1 else 0
@@ -452,8 +476,7 @@ class PPOTrainer:
             e = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
                           amp=self.amp, fused=self.fused, sync=False)
             parts = e if parts is None else parts + e
-        progress = min(1.0, self.total_episodes / ENTROPY_ANNEAL_EPISODES)       # ppo_agent.py:193-197
-        self.entropy_coef = ENTROPY_COEF_START - progress * (ENTROPY_COEF_START - ENTROPY_COEF_END)
+        self.entropy_coef = entropy_coef_after_update(self.entropy_anneal, self.total_episodes)
         p = (parts / NUM_EPOCHS).tolist()
         return {"policy_loss": p[0], "value_loss": p[1], "entropy": p[2], "total_loss": p[3]}
 
@@ -489,6 +512,7 @@ def main():
     ap.add_argument("--metrics", default=None)
     ap.add_argument("--save", default=None)
     ap.add_argument("--returns", default="lane", choices=["lane", "reference"])
+    ap.add_argument("--entropy-anneal", default="train", choices=["train", "train_single"])
     args = ap.parse_args()
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
@@ -500,7 +524,7 @@ def main():
         else:
             dist.init_process_group(backend)
     tr = PPOTrainer(batch=args.batch, horizon=args.horizon, hidden=args.hidden, seed=args.seed,
-                    returns=args.returns)
+                    returns=args.returns, entropy_anneal=args.entropy_anneal)
     for u in range(args.updates):
         m = tr.iteration()
         m["update"] = u

@@ -38,4 +38,8 @@ def run_parallel(seconds: float, procs: int):
     import multiprocessing as mp
     with mp.get_context("spawn").Pool(procs) as pool:
         res = pool.map(_worker, [(seconds, k) for k in range(procs)])
+        # let the workers exit on their own: leaving the with-block while they are
+        # alive terminates them with SIGTERM (abort dumps under rocprofv3)
+        pool.close()
+        pool.join()
     return sum(r[0] for r in res), sum(r[1] for r in res)

@@ -243,3 +243,24 @@ def test_episode_stats_match_reference_loop():
         for k in EPISODE_STATS:
             assert got[k] == pytest.approx(want[k], abs=1e-9), k
         np.testing.assert_allclose(carry.numpy(), np.array(ref_acc), atol=1e-12)
+
+
+def test_entropy_anneal_modes():
+    """train.py never increments agent.total_episodes (it counts a module global,
+    train.py:74), so ppo_agent.py:193-197 keeps the coefficient at 0.15; under
+    train_single.py (agent.total_episodes += 1 per episode, :78) it anneals
+    linearly to 0.01 over 400,000 episodes.  The reference agent class's own
+    update_entropy_coef gives the train_single values for a counted episode total."""
+    from bgx.train import entropy_coef_after_update
+    from bgx.ppo import ENTROPY_COEF_START, ENTROPY_COEF_END, ENTROPY_ANNEAL_EPISODES
+    agent = BackgammonPPOAgent(action_size=500, device=torch.device("cpu"))
+    for eps in (0, 1, 65_536, 200_000, 399_999, 400_000, 10_000_000):
+        assert entropy_coef_after_update("train", eps) == ENTROPY_COEF_START
+        agent.total_episodes = eps
+        agent.update_entropy_coef()
+        assert entropy_coef_after_update("train_single", eps) == agent.entropy_coef
+    assert entropy_coef_after_update("train_single", ENTROPY_ANNEAL_EPISODES // 2) == pytest.approx(0.08)
+    assert entropy_coef_after_update("train_single", 10 ** 9) == pytest.approx(ENTROPY_COEF_END)
+    import inspect
+    from bgx.train import PPOTrainer
+    assert inspect.signature(PPOTrainer).parameters["entropy_anneal"].default == "train"

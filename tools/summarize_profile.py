@@ -1,5 +1,7 @@
-"""Summarize a tools/profile.sh run: per-kernel stats + HBM traffic per launch of
-the dominant kernels.
+"""Summarize a tools/profile.sh run: per-kernel stats, HBM traffic per launch of
+the env-step kernels, the env step's SQ instruction mix and wave-cycle split
+(the issue-rate roofline), and every 2-ply evaluator k_eval<*> with its OWN
+counter rows (MFMA busy, VALU, HBM read).
 
 FETCH_SIZE calibration (MI355X_MICROARCH.md §HBM: the guide's x2 correction is
 for 16-B-per-lane streaming reads; "other access widths are uncalibrated:
@@ -9,27 +11,42 @@ step's access shapes -- a 64-B lane record read 1 B per lane, 4-/8-B scalar
 reads, 4-/8-B and 64-B stores -- are each ONE 64-B EA request that FETCH_SIZE
 tallies at 64 B, so the env-step kernels' bytes are (FETCH_SIZE + WRITE_SIZE)
 x 1024, not doubled; the 2-ply evaluator's 16-B-per-lane pool stream keeps the
-guide's doubling."""
+guide's doubling.
+
+Usage: python tools/summarize_profile.py OUT "bench args" "pmc bench args"
+"""
 import csv
 import json
 import os
 import statistics
 import sys
 
+CLOCK_GHZ = 2.4          # MI355X peak engine clock (MI355X_MICROARCH.md chip table)
+CUS, SIMDS = 256, 1024
+
 out, cmd = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "")
 pmc_cmd = sys.argv[3] if len(sys.argv) > 3 else cmd
 stats = list(csv.DictReader(open(os.path.join(out, "trace", "run_kernel_stats.csv"))))
 
 
-def pmc(kind, counter):
+def short(name):
+    return name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+
+
+def pmc_rows(kind):
+    """{kernel name: {counter: [value per dispatch]}} of one --pmc pass."""
     res = {}
     p = os.path.join(out, kind, "run_counter_collection.csv")
     if not os.path.exists(p):
         return res
     for r in csv.DictReader(open(p)):
-        if r["Counter_Name"] == counter:
-            res.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
+        d = res.setdefault(r["Kernel_Name"], {})
+        d.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return res
+
+
+def pmc(kind, counter):
+    return {n: v[counter] for n, v in pmc_rows(kind).items() if counter in v}
 
 
 fetch, write = pmc("fetch", "FETCH_SIZE"), pmc("write", "WRITE_SIZE")
@@ -37,59 +54,133 @@ kernels = []
 for s in stats:
     name = s["Name"]
     k = {"name": name, "calls": int(s["Calls"]), "avg_ns": float(s["AverageNs"]), "pct": float(s["Percentage"])}
-    f = next((v for n, v in fetch.items() if n == name), None)
-    w = next((v for n, v in write.items() if n == name), None)
+    f, w = fetch.get(name), write.get(name)
     if f and w:
         k["FETCH_SIZE_KiB"] = statistics.mean(f)
         k["WRITE_SIZE_KiB"] = statistics.mean(w)
         k["hbm_bytes_per_launch"] = (k["FETCH_SIZE_KiB"] + k["WRITE_SIZE_KiB"]) * 1024   # calibrated, see top
     kernels.append(k)
-# per-dispatch durations of the dominant kernels over the timed tail (last --steps launches)
-tail = None
-for tok in cmd.split():
-    pass
 args = cmd.split()
-if "--steps" in args:
-    tail = int(args[args.index("--steps") + 1])
+tail = int(args[args.index("--steps") + 1]) if "--steps" in args else None
 trace = list(csv.DictReader(open(os.path.join(out, "trace", "run_kernel_trace.csv"))))
 for k in kernels[:4]:
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in trace if r["Kernel_Name"] == k["name"]]
     if tail and len(d) >= tail:
         k["avg_ns_timed_tail"] = statistics.mean(d[-tail:])
+
+# ---------------------------------------------------------------- env step --
 # the env step = every kernel bgx_step launches once per step (Philox split dispatch):
-# both k_step launches, the dispatch-order sort, and the overflow tiers.  Their
-# durations are averaged over the C3 (B = 65,536) dispatches only: the default bench
-# also runs C2 at B = 4,096 with the same kernels, told apart by grid size.
+# both k_step launches, the dispatch-order sort, and the overflow tiers.  Durations are
+# averaged over the C3 (B = 65,536) dispatches only: the default bench also runs C2 at
+# B = 4,096 with the same kernels, told apart by grid size.
 STEP_KERNELS = ("k_step<0", "k_order_count", "k_order_scatter", "k_movegen_over<0")
 env = {"kernels": [], "hbm_bytes_per_step": 0.0, "busy_ns_per_step": 0.0}
 for k in kernels:
-    short = k["name"].replace("(anonymous namespace)::", "").replace("void ", "")
-    if any(short.startswith(p) for p in STEP_KERNELS):
+    sh = short(k["name"])
+    if any(sh.startswith(p) for p in STEP_KERNELS):
         rows = [r for r in trace if r["Kernel_Name"] == k["name"]]
         gmax = max(int(r["Grid_Size_X"]) for r in rows)
         big = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows if int(r["Grid_Size_X"]) * 4 >= gmax]
-        if short.startswith("k_step<0"):
+        if sh.startswith("k_step<0"):
             k["avg_ns_c3"] = statistics.mean(big)
-        env["kernels"].append({"name": short.split("(")[0], "avg_ns": k.get("avg_ns_c3", k["avg_ns"]),
+        env["kernels"].append({"name": sh, "avg_ns": k.get("avg_ns_c3", k["avg_ns"]),
                                "hbm_bytes_per_launch": k.get("hbm_bytes_per_launch")})
         env["busy_ns_per_step"] += k.get("avg_ns_c3", k["avg_ns"])
         env["hbm_bytes_per_step"] += k.get("hbm_bytes_per_launch") or 0.0
-# 2-ply evaluator (k_eval): MFMA busy cycles (SQ_VALU_MFMA_BUSY_CYCLES counts cycles,
-# 32 per v_mfma_f32_32x32x16; MI355X_MICROARCH.md constants table) over 1024 SIMDs x
-# the kernel's duration at 2.4 GHz, and its HBM read bytes (2 x FETCH_SIZE KiB)
-ev = {}
-mf = pmc("mfma", "SQ_VALU_MFMA_BUSY_CYCLES")
-ef = pmc("efetch", "FETCH_SIZE")
-ek = next((k for k in kernels if "k_eval" in k["name"]), None)
-if ek and mf:
-    busy = statistics.mean(next(iter(mf.values())))
-    ev = {"kernel": ek["name"], "avg_ns": ek["avg_ns"], "mfma_busy_cycles": busy,
-          "mfma_busy_frac_at_2p4GHz": busy / (1024 * ek["avg_ns"] * 2.4)}
-    if ef:
-        ev["hbm_read_bytes"] = 2 * statistics.mean(next(iter(ef.values()))) * 1024
+
+# SQ passes of the C3 step alone ("sqi": instruction counts, "sqc": wave-cycle split).
+# Both passes run the same command, so per-pass totals over all env-step dispatches /
+# the lane-steps of that run give per-lane-step figures; the lane-steps are counted as
+# k_order_count dispatches (one per shard step) x lanes per shard.
+lanes_per_shard = None
+if "--batch" in pmc_cmd.split():
+    pa = pmc_cmd.split()
+    lanes_per_shard = int(pa[pa.index("--batch") + 1]) // int(pa[pa.index("--shards") + 1] if "--shards" in pa else 2)
+else:
+    lanes_per_shard = 65536 // 2
+sq = {}
+for kind in ("sqi", "sqc"):
+    rows = pmc_rows(kind)
+    if not rows:
+        continue
+    shard_steps = len(next((v["SQ_WAVES"] for n, v in rows.items() if "k_order_count" in n), []))
+    tot = {}
+    for n, v in rows.items():
+        if not any(short(n).startswith(p) for p in STEP_KERNELS):
+            continue
+        for c, vals in v.items():
+            if c.startswith("SQ_") and c != "SQ_WAVES":
+                tot[c] = tot.get(c, 0.0) + sum(vals)
+    if shard_steps:
+        sq[kind] = {"shard_steps": shard_steps, "per_lane_step": {c: t / (shard_steps * lanes_per_shard)
+                                                                   for c, t in tot.items()}}
+if sq:
+    ins = sq.get("sqi", {}).get("per_lane_step", {})
+    cyc = sq.get("sqc", {}).get("per_lane_step", {})
+    env["sq"] = {"lanes_per_shard_step": lanes_per_shard, "instructions_per_lane_step": ins,
+                 "quad_cycles_per_lane_step": cyc}
+    if cyc.get("SQ_WAVE_CYCLES"):
+        wc = cyc["SQ_WAVE_CYCLES"]
+        env["sq"]["wave_time_split"] = {
+            "active_any": cyc.get("SQ_ACTIVE_INST_ANY", 0) / wc,
+            "wait_any (s_waitcnt / barrier: memory + LDS latency)": cyc.get("SQ_WAIT_ANY", 0) / wc,
+            "wait_inst_any (issue stall)": cyc.get("SQ_WAIT_INST_ANY", 0) / wc,
+            "wait_inst_lds (LDS issue stall, part of wait_inst_any)": cyc.get("SQ_WAIT_INST_LDS", 0) / wc,
+            "active_valu": cyc.get("SQ_ACTIVE_INST_VALU", 0) / wc,
+            "active_lds": cyc.get("SQ_ACTIVE_INST_LDS", 0) / wc}
+    # issue-pipe capacities (cycles a unit is occupied per wave-instruction / units on the chip):
+    # VALU wave64 = 2 cycles on a SIMD-32 (MI355X_MICROARCH.md "Wave scheduling"), 1,024 SIMDs;
+    # SALU one instruction per cycle on each CU's single scalar unit (chip table "CU"), 256;
+    # LDS one instruction issued per cycle per CU (a floor: wide accesses take more), 256;
+    # SMEM / VMEM / branch one per cycle per CU each.
+    if ins:
+        env["sq"]["pipe_model"] = {"VALU": {"counter": "SQ_INSTS_VALU", "cycles_per_inst": 2, "units": SIMDS},
+                                   "SALU": {"counter": "SQ_INSTS_SALU", "cycles_per_inst": 1, "units": CUS},
+                                   "LDS": {"counter": "SQ_INSTS_LDS", "cycles_per_inst": 1, "units": CUS},
+                                   "SMEM": {"counter": "SQ_INSTS_SMEM", "cycles_per_inst": 1, "units": CUS},
+                                   "VMEM": {"counter": "SQ_INSTS_VMEM", "cycles_per_inst": 1, "units": CUS},
+                                   "BRANCH": {"counter": "SQ_INSTS_BRANCH", "cycles_per_inst": 1, "units": CUS}}
+        env["sq"]["clock_ghz"] = CLOCK_GHZ
+        # unit-busy ns per shard step if that pipe alone bound the step
+        env["sq"]["pipe_bound_ns_per_shard_step"] = {
+            p: ins.get(m["counter"], 0.0) * lanes_per_shard * m["cycles_per_inst"] / m["units"] / CLOCK_GHZ
+            for p, m in env["sq"]["pipe_model"].items()}
+
+# ------------------------------------------------------------ 2-ply k_eval --
+# every evaluator instantiation separately (k_eval<3> = H 40, k_eval<8> = H 128), each
+# with its own counter rows: MFMA busy cycles (SQ_VALU_MFMA_BUSY_CYCLES counts cycles,
+# 32 per v_mfma_f32_32x32x16; MI355X_MICROARCH.md constants table) over 1,024 SIMDs x
+# its duration at 2.4 GHz; VALU instructions / active quad-cycles; HBM read bytes
+# (2 x FETCH_SIZE KiB, the guide's 16-B streaming correction)
+mrows, erows = pmc_rows("mfma"), pmc_rows("efetch")
+evals = []
+for k in kernels:
+    if "k_eval<" not in k["name"]:
+        continue
+    e = {"kernel": short(k["name"]), "avg_ns": k["avg_ns"], "calls": k["calls"]}
+    m = mrows.get(k["name"], {})
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+        busy = statistics.mean(m["SQ_VALU_MFMA_BUSY_CYCLES"])
+        e["mfma_busy_cycles"] = busy
+        e["mfma_busy_frac_at_2p4GHz"] = busy / (SIMDS * k["avg_ns"] * CLOCK_GHZ)
+    for c in ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_MFMA", "SQ_WAVE_CYCLES", "SQ_WAVES",
+              "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
+        if c in m:
+            e[c] = statistics.mean(m[c])
+    if "SQ_INSTS_VALU" in e:      # VALU pipe busy (2 cycles per wave64 instruction, MFMA included)
+        e["valu_issue_frac_at_2p4GHz"] = e["SQ_INSTS_VALU"] * 2 / (SIMDS * k["avg_ns"] * CLOCK_GHZ)
+    f = erows.get(k["name"], {}).get("FETCH_SIZE")
+    if f:
+        e["hbm_read_bytes"] = 2 * statistics.mean(f) * 1024
+    evals.append(e)
+
 summary = {"command": "python bench.py " + cmd, "pmc_command": "python bench.py " + pmc_cmd,
-           "kernels": kernels[:20], "env_step": env, "two_ply_eval": ev}
+           "kernels": kernels[:24], "env_step": env, "two_ply_eval": evals}
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
-for k in kernels[:20]:
+for k in kernels[:24]:
     print(f"{k['pct']:6.2f}% {k['avg_ns']/1e3:10.1f} us (tail {k.get('avg_ns_timed_tail', 0)/1e3:.1f}) "
           f"x{k['calls']:4d}  {k['name'][:70]}  {k.get('hbm_bytes_per_launch', 0)/1e6:.1f} MB")
+if "sq" in env:
+    print(json.dumps(env["sq"], indent=1))
+for e in evals:
+    print(json.dumps(e))
