@@ -174,6 +174,15 @@ for k in kernels:
         e["hbm_read_bytes"] = 2 * statistics.mean(f) * 1024
     evals.append(e)
 
+# per-pass, per-kernel counter totals and dispatch counts (the raw CSVs reduced, so the
+# figures above can be recomputed from what is committed under profiles/)
+with open(os.path.join(out, "pmc_totals.csv"), "w") as fo:
+    fo.write("pass,kernel,counter,dispatches,total\n")
+    for kind in ("fetch", "write", "sqi", "sqc", "mfma", "efetch"):
+        for n, v in pmc_rows(kind).items():
+            for c, vals in v.items():
+                fo.write(f"{kind},{short(n).replace(',', ';')},{c},{len(vals)},{sum(vals):.17g}\n")
+
 summary = {"command": "python bench.py " + cmd, "pmc_command": "python bench.py " + pmc_cmd,
            "kernels": kernels[:24], "env_step": env, "two_ply_eval": evals}
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
