@@ -251,6 +251,36 @@ int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* st
 int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_dev, const void* b1h_dev,
                     int32_t hidden, void* h_dev, void* stream);
 
+/* The fp16 epoch's output layer + loss head without materialised logits
+ * (csrc/bg_ppo_fused.hip; replaces, inside ppo_agent.py:268-305 under autocast,
+ * the [action_head; value_head] GEMM of policy_network.py:71-75, the loss head of
+ * bgx_ppo_head_ex, dh = dy W2h, the ReLU backward and gW2 / gb2 = dy^T [h | 1]).
+ * hidden = 128, n_actions = 500; W2h [512][128] fp16 = [action_head.weight;
+ * value_head.weight; 0] and b2h [512] fp16 likewise; h [m][128] fp16 = the fc1
+ * output (bgx_fc1_records).  perm [m] lists the rows in ascending order of the
+ * number of 32-action tiles they need (ceil(cnt / 32), 16 for cnt = 0; any order
+ * is correct, sorted is fast).
+ * bgx_ppo_rows: per row the loss parts (added to sums[0..2] as bgx_ppo_head),
+ * dh [m][128] fp16 = ReLU'(h) * fp16(dy W2h) (original row order), and the row
+ * statistics stats [m] (16 B, 16-byte aligned) + info [m] (int32) in perm order
+ * for bgx_ppo_gw2; dy_or_null [m][512] fp16 receives dy = [dlogits | dvalue | 0]
+ * (tests).  grid <= 0: 256 workgroups.
+ * bgx_ppo_gw2: gw2 [512][128] += dy^T h and gb2 [512] += column sums of dy (fp32),
+ * dy recomputed from the statistics; plan int32[33] = task prefix per action tile
+ * (17 entries, tasks of BGX_PPO_GW2_TASK_TILES row tiles) then the first row tile
+ * (of perm order) each action tile needs (16); workspace of
+ * bgx_ppo_gw2_workspace(m) bytes. */
+#define BGX_PPO_GW2_TASK_TILES 32
+int bgx_ppo_rows(const void* h_dev, const int32_t* perm_dev, const uint8_t* records_dev, const int32_t* actions_dev,
+                 const float* old_logp_dev, const float* returns_dev, const float* adv_dev, int32_t m, int32_t hidden,
+                 int32_t n_actions, const void* w2h_dev, const void* b2h_dev, float eps_clip, float c_value,
+                 float c_entropy, float grad_scale, void* dh_dev, void* stats_dev, int32_t* info_dev,
+                 double* sums_dev, void* dy_or_null, int32_t grid, void* stream);
+int64_t bgx_ppo_gw2_workspace(int32_t m);
+int bgx_ppo_gw2(const void* h_dev, const int32_t* perm_dev, const void* stats_dev, const int32_t* info_dev, int32_t m,
+                int32_t hidden, int32_t n_actions, const void* w2h_dev, const void* b2h_dev, float k1,
+                const int32_t* plan_dev, float* workspace_dev, float* gw2_dev, float* gb2_dev, void* stream);
+
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
  * evaluation after it (k_eval, the MFMA kernel). */

@@ -39,6 +39,7 @@ import json
 import os
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -286,7 +287,7 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
             w1pack = torch.empty(L.bgx_fc1_packed_size(Hd), dtype=torch.uint8, device=dev)
             check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
         hsum = torch.empty(RELU_BLOCKS, Hd, dtype=torch.float32, device=dev)
-        for feats, legal, actions, old_logp, returns, adv, records in chunks:
+        for feats, legal, actions, old_logp, returns, adv, records, *_ in chunks:
             x = feats.half()
             if x.shape[1] != F_in and Kw is None:   # zero-padded rows: zero weight columns to match
                 Kw = x.shape[1]
@@ -325,6 +326,105 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
     wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
 
 
+PPO_GW2_TASK_TILES = 32        # include/bgx.h BGX_PPO_GW2_TASK_TILES
+# The fp16 epoch's output layer + loss head as two HIP kernels without materialised
+# logits (csrc/bg_ppo_fused.hip); BGX_PPO_FUSED=0 keeps the round-2 manual epoch
+# (hipBLASLt head GEMM + bgx_ppo_head_ex + dy W2h + ReLU backward + split-K gW2) for A/B.
+PPO_FUSED_HEAD = os.environ.get("BGX_PPO_FUSED", "1") != "0"
+FEAT_BIAS_COL = 198            # the ones column of the 208-wide rows: gW1[:, 198] = gb1
+
+
+def ppo_row_plan(records: torch.Tensor, n_actions: int = 500):
+    """Row order and work plan of bgx_ppo_rows / bgx_ppo_gw2 for one chunk of
+    rollout rows (computed once per update; the records do not change across
+    epochs).  A row needs the 32-action tiles holding its legal columns
+    (ceil(cnt / 32); all 16 when cnt = 0, every action then being masked by the
+    same constant); rows are sorted by that count (stable).  plan = the k_ppo_gw2
+    task prefix per action tile (17) and the first row tile (in sorted order) that
+    reaches each action tile (16).  Device tensors only: no host sync."""
+    m = records.shape[0]
+    cnt = records[:, 60].to(torch.int32) | (records[:, 61].to(torch.int32) << 8)
+    lim = torch.where(cnt == 0, torch.full_like(cnt, n_actions), cnt.clamp(max=n_actions))
+    cls = ((lim + 31) // 32).to(torch.uint8)
+    perm = torch.argsort(cls, stable=True).to(torch.int32)
+    cum = torch.cumsum(torch.bincount(cls, minlength=17), 0)
+    start = torch.div(cum[:16], 32, rounding_mode="floor")
+    start[15] = 0                                     # the value column's tile: every row
+    ntiles = (m + 31) // 32
+    tasks = (ntiles - start + PPO_GW2_TASK_TILES - 1) // PPO_GW2_TASK_TILES
+    pre = torch.cat([torch.zeros(1, dtype=tasks.dtype, device=tasks.device), torch.cumsum(tasks, 0)])
+    return perm, torch.cat([pre, start]).to(torch.int32).contiguous()
+
+
+def _fused_head_ok(net) -> bool:
+    return PPO_FUSED_HEAD and net.fc1.out_features == 128 and net.action_head.out_features == 500
+
+
+def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
+    """The fp16-autocast epoch with the output layer and loss head fused
+    (bgx_ppo_rows + bgx_ppo_gw2): fc1 from the records (bgx_fc1_records), then per
+    row the logits, the loss head, dy and dh = ReLU'(h) fp16(dy W2h) on MFMA without
+    the [n, 512] logits in HBM; gW2 / gb2 = dy^T [h | 1] from per-row statistics;
+    gW1 / gb1 = dh^T [x | 1] (the ones column of the 208-wide feature rows).  Same
+    fp16 operands, fp32 accumulation and per-row gradient scaling as
+    _ppo_epoch_amp_manual; gradients land in p.grad as fp32."""
+    eps, c_v, c_e, gscale = coefs
+    row_scale = gscale * n_total / min(n_total, REF_ROWS)
+    post = min(n_total, REF_ROWS) / n_total
+    W1, b1 = net.fc1.weight, net.fc1.bias
+    Wa, ba = net.action_head.weight, net.action_head.bias
+    wv, bv = net.value_head.weight, net.value_head.bias
+    A, Hd = Wa.shape
+    F_in = W1.shape[1]
+    dev = W1.device
+    k1 = float(np.float32(row_scale) * np.float32(c_e))      # the kernel's fp32 gscale * c_entropy
+    with torch.no_grad():
+        W1h, b1h = W1.half(), b1.half()
+        W2h = torch.zeros(512, Hd, dtype=torch.float16, device=dev)
+        b2h = torch.zeros(512, dtype=torch.float16, device=dev)
+        W2h[:A] = Wa.half(); W2h[A] = wv[0].half()
+        b2h[:A] = ba.half(); b2h[A] = bv[0].half()
+        gW1 = torch.zeros(Hd, 208, dtype=torch.float32, device=dev)
+        gW2 = torch.zeros(512, Hd, dtype=torch.float32, device=dev)
+        gb2 = torch.zeros(512, dtype=torch.float32, device=dev)
+        L = _lib.load()
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        w1pack = torch.empty(L.bgx_fc1_packed_size(Hd), dtype=torch.uint8, device=dev)
+        check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
+        for feats, _legal, actions, old_logp, returns, adv, records, *extra in chunks:
+            prep = extra[0] if extra else {}
+            rec = records.contiguous()
+            m = rec.shape[0]
+            if prep.get("bias_col"):                # 208-wide fp16 rows with ones in column 198
+                x = feats
+            else:
+                x = torch.zeros(m, 208, dtype=torch.float16, device=dev)
+                x[:, :F_in] = feats[:, :F_in]
+                x[:, FEAT_BIAS_COL] = 1.0
+            perm, plan = prep["plan"] if "plan" in prep else ppo_row_plan(rec, A)
+            h = torch.empty(m, Hd, dtype=torch.float16, device=dev)
+            check(L.bgx_fc1_records(p(rec), m, p(w1pack), p(b1h), Hd, p(h), stream), "bgx_fc1_records")
+            dh = torch.empty(m, Hd, dtype=torch.float16, device=dev)
+            stats = torch.empty(m, 4, dtype=torch.float32, device=dev)
+            info = torch.empty(m, dtype=torch.int32, device=dev)
+            acts = actions.to(torch.int32).contiguous()
+            old, ret, ad = old_logp.float().contiguous(), returns.float().contiguous(), adv.float().contiguous()
+            check(L.bgx_ppo_rows(p(h), p(perm), p(rec), p(acts), p(old), p(ret), p(ad), m, Hd, A, p(W2h), p(b2h),
+                                 eps, c_v, c_e, row_scale, p(dh), p(stats), p(info), p(sums), None, 0, stream),
+                  "bgx_ppo_rows")
+            ws = torch.empty(L.bgx_ppo_gw2_workspace(m) // 4, dtype=torch.float32, device=dev)
+            check(L.bgx_ppo_gw2(p(h), p(perm), p(stats), p(info), m, Hd, A, p(W2h), p(b2h), k1, p(plan), p(ws),
+                                p(gW2), p(gb2), stream), "bgx_ppo_gw2")
+            gW1 += _wgrad(dh, x)
+        if post != 1.0:
+            for t in (gW1, gW2, gb2):
+                t.mul_(post)
+    W1.grad, b1.grad = gW1[:, :F_in].contiguous(), gW1[:, FEAT_BIAS_COL].contiguous()
+    Wa.grad, ba.grad = gW2[:A].contiguous(), gb2[:A].contiguous()
+    wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
+
+
 def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync=True):
     dev = next(net.parameters()).device
     if scaler.is_enabled():
@@ -336,9 +436,12 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
     coefs = (EPS_CLIP, VALUE_LOSS_COEF, float(entropy_coef), float(scale) / n_total)
     manual = amp and os.environ.get("BGX_PPO_MANUAL", "1") != "0" and _is_policy_mlp(net)
     if manual:
-        _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums)
+        if _fused_head_ok(net):
+            _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums)
+        else:
+            _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums)
         chunks = ()
-    for feats, legal, actions, old_logp, returns, adv, records in chunks:
+    for feats, legal, actions, old_logp, returns, adv, records, *_ in chunks:
         with autocast(device_type=dev.type, enabled=amp):
             logits, values = net(feats)
         out = _PPOHead.apply(logits, values, records.contiguous(), actions.to(torch.int32).contiguous(),
@@ -458,9 +561,15 @@ class PPOTrainer:
         # the fused path's features are encoded once and kept for the 4 epochs
         # (fp16 under autocast: 2^21 rows x 198 x 2 B = 0.8 GB of HBM)
         manual = self.fused and self.amp and os.environ.get("BGX_PPO_MANUAL", "1") != "0" and _is_policy_mlp(self.net)
+        fused_head = manual and _fused_head_ok(self.net)
         feats = [encode_records(recs[s:min(N, s + self.chunk)], torch.float16 if self.amp else torch.float32,
-                                width=FEAT_W if manual else 198)
+                                width=208 if fused_head else (FEAT_W if manual else 198))
                  for s in range(0, N, self.chunk)] if self.fused else None
+        preps = [{} for _ in range(0, N, self.chunk)]
+        if fused_head:      # the ones column (fc1's bias gradient) and the row plan, once per update
+            for i, s in enumerate(range(0, N, self.chunk)):
+                feats[i][:, FEAT_BIAS_COL] = 1.0
+                preps[i] = {"bias_col": True, "plan": ppo_row_plan(recs[s:min(N, s + self.chunk)], self.A)}
 
         def chunks():
             for i, s in enumerate(range(0, N, self.chunk)):
@@ -469,7 +578,7 @@ class PPOTrainer:
                     f, legal = feats[i], None
                 else:
                     f, legal = features_and_masks(recs[s:e], self.A)
-                yield f, legal, acts[s:e], old[s:e], R[s:e], adv[s:e], recs[s:e]
+                yield f, legal, acts[s:e], old[s:e], R[s:e], adv[s:e], recs[s:e], preps[i]
 
         parts = None
         for _ in range(NUM_EPOCHS):

@@ -1,0 +1,533 @@
+// bg_ppo_fused.hip — the fp16 (autocast) PPO epoch's output layer and loss head
+// (ppo_agent.py:268-305 under autocast, policy_network.py:71-75) without the
+// [n, 512] logits or their gradient ever reaching HBM.
+//
+// The round-2 epoch ran, per 2^20-row chunk, a hipBLASLt GEMM writing the fp16
+// logits y = h W2h^T + b2h ([action_head; value_head; 0], 512 columns), the loss
+// head reading them and writing dy (2 GiB of HBM traffic), dh = dy W2h, the ReLU
+// backward and gW2 = dy^T h.  Here:
+//
+//  * k_ppo_rows — one wave per 32 rows, W2h (128 KiB) in LDS for the workgroup's
+//    life.  Z^T = W2h h^T on v_mfma_f32_32x32x16_f16 (lane = row, 16 logits per
+//    lane and 32-action tile), rounded to fp16 and kept packed in registers; the
+//    masked log-softmax, the clipped surrogate, the value error and the entropy
+//    run in registers (one cross-half shuffle per row reduction); the gradient
+//    dz = dL/dy (fp16, exactly as the loss-head kernel bgx_ppo_head_ex forms it)
+//    is consumed UNMOVED as the B operand of dh^T = W2h^T dz^T (W2h^T read from
+//    the same LDS image with ds_read_b64_tr_b16), the ReLU mask applied, and dh
+//    stored.  Per row it writes 20 bytes of statistics for the second kernel.
+//  * k_ppo_gw2 — gW2 = dz^T h needs dz with the ROW on the reduction axis, i.e.
+//    the other orientation: Z = h W2h^T for one 32-action tile per wave (lane =
+//    action), dz recomputed from the row statistics (bit-identical formulas),
+//    and dz^T h accumulated over the wave's rows (h^T from a per-wave LDS tile
+//    via ds_read_b64_tr_b16); the bias gradient gb2 is the row sum of dz in the
+//    lane.  Per-task partials are summed by k_ppo_gw2_reduce (deterministic).
+//
+// Sparsity (exact): a row with cnt >= 1 legal actions has masked logits at
+// z + log(1e-45) (ppo_agent.py:166), i.e. probabilities below 1e-44 relative:
+// their fp16 gradients are exactly 0 (fp16's smallest subnormal is 6e-8) and their
+// entropy / log-sum-exp terms lie 40 orders of magnitude below fp32 resolution.
+// So a row needs only the action tiles holding its legal columns, plus the tile
+// holding the value column; a row with no legal action (all 500 masked by the same
+// constant: softmax is shift-invariant) needs all 16.  Rows are sorted by that
+// tile count (host side, once per update), so a wave's 32 rows need the same tiles
+// and k_ppo_gw2 visits, for action tile a, only the rows that reach it.  Mean
+// legal count in self-play is ~19, so most rows need 2 of the 16 tiles.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "../../include/bgx.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((__vector_size__(4 * sizeof(short))));
+
+constexpr int kA = 500;                 // action_size (agent/config.py; max_legal_moves)
+constexpr int kAp = 512;                // [action_head; value_head; zero rows]
+constexpr int kH = 128;                 // hidden_size (agent/config.py:8)
+constexpr int kNT = kAp / 32;           // 16 action tiles
+constexpr int kVT = kA / 32;            // 15: the tile holding the value column kA
+constexpr int kVr = kA - 32 * kVT;      // its row in the tile (20)
+constexpr int kVi = (kVr & 3) + 4 * (kVr >> 3);   // accumulator register holding it (8)
+constexpr int kVh = (kVr >> 2) & 1;               // on lane half kVh (1)
+constexpr int kTS = BGX_PPO_GW2_TASK_TILES;       // row tiles per k_ppo_gw2 task
+constexpr int kPart = 32 * kH + 32;               // floats per task partial (gW2 tile + gb2 tile)
+
+constexpr float kL2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+// fp32 log(eps) and log(1 - eps), eps = FLT_EPSILON (torch clamp_probs bounds)
+constexpr float kLogEps = -15.942384719848633f;
+constexpr float kLog1mEps = -1.1920930376163597e-07f;
+
+__device__ __forceinline__ f16x8 as_h8(uint4 v) { return __builtin_bit_cast(f16x8, v); }
+
+// byte offset of 16-byte chunk ch (0..15) of row `row` in an LDS image of 256-byte
+// rows, XOR-swizzled so that both the row reads (ds_read_b128) and the transposed
+// reads (ds_read_b64_tr_b16) of the 32x32x16 operands are bank-conflict free
+// (cdna_hip_programming.md T10, layout (b))
+__device__ __forceinline__ uint32_t swz(int row, int ch) {
+    return 256u * (uint32_t)row + 16u * (uint32_t)(ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ s16x4 tr16(const uint8_t* lds) {
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(__attribute__((address_space(3))) void*)lds);
+}
+
+// The 32x32x16 operand whose lane is column n = l & 31 of a [k][n] tile held
+// row-major in a swizzled LDS image of 256-byte rows: element j of lane half hh is
+// row 16s + 8(j >> 2) + 4hh + (j & 3) -- the k order in which an accumulator's
+// registers 8s..8s+7 deliver their rows -- at column 32u + n.  Two transposed reads
+// (rows +0..3 and +8..11 of the half's block).  Image rows start at `row0`.
+// `l` is the lane id, passed laundered by callers inside unrolled loops so that LLVM
+// recomputes these few address instructions per use instead of hoisting every
+// (tile, s, u) combination into registers of its own.
+__device__ __forceinline__ int laundered_lane() {
+    int l = (int)(threadIdx.x & 63);
+    __asm__ volatile("" : "+v"(l));
+    return l;
+}
+__device__ __forceinline__ f16x8 tr_operand(const uint8_t* img, int row0, int s, int u, int l) {
+    const int g = l >> 4, q = (l & 15) >> 2, p = l & 3;
+    const int r = row0 + 16 * s + 4 * (g >> 1) + q;
+    const int ch = 4 * u + 2 * (g & 1) + (p >> 1);
+    // whole-register casts: element-wise short -> _Float16 inserts were lowered to
+    // v_perm sequences that dropped the upper dword of each read
+    const uint2 a = __builtin_bit_cast(uint2, tr16(img + swz(r, ch) + 8 * (p & 1)));
+    const uint2 b = __builtin_bit_cast(uint2, tr16(img + swz(r + 8, ch) + 8 * (p & 1)));
+    return __builtin_bit_cast(f16x8, make_uint4(a.x, a.y, b.x, b.y));
+}
+
+__device__ __forceinline__ float hsum(float v) { return v + __shfl_xor(v, 32); }
+
+// the loss head's per-element quantities (bgx_ppo_head_ex's formulas): tz = the
+// logit in log2 units or -inf when out of play; u = natural log-prob; lp = its
+// clamp to [log eps, log(1 - eps)] (torch clamp_probs); p; q = lp + [not clamped]
+struct Elem {
+    float u, lp, p, q;
+};
+__device__ __forceinline__ Elem elem(float tz, float lse2, float nlse) {
+    Elem e;
+    e.u = fmaf(tz, kLn2, nlse);
+    e.lp = fminf(fmaxf(e.u, kLogEps), kLog1mEps);
+    e.p = __builtin_amdgcn_exp2f(tz - lse2);
+    e.q = e.lp + (e.lp == e.u ? 1.0f : 0.0f);
+    return e;
+}
+
+struct RowsArgs {
+    const _Float16* h;          // [m][128] fc1 output (fp16, after ReLU), original row order
+    const int32_t* perm;        // sorted position -> original row
+    const uint8_t* recs;        // [m][64] lane records (legal count at bytes 60-61)
+    const int32_t* act;
+    const float* old_logp;
+    const float* ret;
+    const float* adv;
+    const _Float16* w2h;        // [512][128] fp16 [action_head; value_head; 0]
+    const _Float16* b2h;        // [512]
+    int m;
+    float eps_clip, c_value, c_entropy, gscale;
+    _Float16* dh;               // [m][128] dL/dh after the ReLU mask, original row order
+    float4* stats;              // [m] sorted order: lse2, k2, gla, gv
+    int32_t* info;              // [m] sorted order: act | lim << 16
+    double* sums;               // policy loss, value error^2, entropy sums
+    _Float16* dy;               // optional [m][512] dL/dy (tests), original row order
+};
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_ppo_rows(RowsArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t sw[kAp * 256];     // W2h, 128 KiB
+    __shared__ __attribute__((aligned(16))) float sb[kAp];
+    __shared__ double red[8][3];
+    for (int i = threadIdx.x; i < kAp * 16; i += blockDim.x)
+        *(uint4*)(sw + swz(i >> 4, i & 15)) = ((const uint4*)a.w2h)[i];
+    for (int i = threadIdx.x; i < kAp; i += blockDim.x) sb[i] = (float)a.b2h[i];
+    __syncthreads();
+
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int r = l & 31, hh = l >> 5;
+    const int ntiles = (a.m + 31) >> 5;
+    const float k1 = a.gscale * a.c_entropy;
+    float s_pol = 0.0f, s_val = 0.0f, s_ent = 0.0f;
+    for (int tile = blockIdx.x * 8 + wv; tile < ntiles; tile += gridDim.x * 8) {
+        const int pos = tile * 32 + r;
+        const bool valid = pos < a.m;
+        const int row = a.perm[valid ? pos : a.m - 1];
+        const uint8_t* rec = a.recs + (size_t)row * 64;
+        const int cnt = (int)rec[60] | ((int)rec[61] << 8);
+        const int lim = cnt == 0 ? kA : (cnt < kA ? cnt : kA);   // columns [0, lim) in play
+        const int act = a.act[row];
+        const float adv = a.adv[row], olp = a.old_logp[row], ret = a.ret[row];
+        int T = (lim + 31) >> 5;                                  // action tiles this row needs
+        #pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) T = max(T, __shfl_xor(T, o));
+        T = __builtin_amdgcn_readfirstlane(T);
+
+        uint4 hf[8];                                              // B operand: h[row][16s + 8hh + j]
+        const uint4* hp = (const uint4*)(a.h + (size_t)row * kH);
+        #pragma unroll
+        for (int s = 0; s < 8; ++s) hf[s] = hp[2 * s + hh];
+        uint32_t hm[4];                                           // bit k: h[row][32u + k] > 0
+        #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            uint32_t own = 0;
+            #pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const uint4 w = hf[2 * u + half];
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+                #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const short b = (short)(ws[j >> 1] >> (16 * (j & 1)));
+                    own |= (b > 0 ? 1u : 0u) << (16 * half + 8 * hh + j);
+                }
+            }
+            hm[u] = own | (uint32_t)__shfl_xor((int)own, 32);
+        }
+
+        // Z^T tiles (lane = row; register i = action 32t + (i&3) + 8(i>>2) + 4hh), fp16
+        f16x2 Z[kNT][8];
+        #pragma unroll
+        for (int t = 0; t < kNT; ++t) {
+            if (t < T || t == kVT) {
+                f32x16 acc;
+                #pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+                const int ll = laundered_lane();
+                #pragma unroll
+                for (int s = 0; s < 8; ++s)
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                        as_h8(*(const uint4*)(sw + swz(32 * t + (ll & 31), 2 * s + (ll >> 5)))), as_h8(hf[s]), acc, 0, 0, 0);
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 bb = *(const float4*)(sb + 32 * t + 8 * q + 4 * hh);
+                    Z[t][2 * q] = f16x2{(_Float16)(acc[4 * q] + bb.x), (_Float16)(acc[4 * q + 1] + bb.y)};
+                    Z[t][2 * q + 1] = f16x2{(_Float16)(acc[4 * q + 2] + bb.z), (_Float16)(acc[4 * q + 3] + bb.w)};
+                }
+                __asm__ volatile("" ::: "memory");       // one tile's LDS reads in flight at a time
+            }
+        }
+        const float v = __shfl((float)Z[kVT][kVi >> 1][kVi & 1], r + 32 * kVh);
+
+// Each pass re-reads the packed fp16 logits: laundering them first keeps LLVM from
+// keeping the fp32 conversions (256 per lane) alive across passes.
+#define BGX_LAUNDER_Z()                                                           \
+        _Pragma("unroll") for (int t = 0; t < kNT; ++t) {                         \
+            if (t < T || t == kVT) {                                              \
+                _Pragma("unroll") for (int q = 0; q < 8; ++q) {                   \
+                    uint32_t w_ = __builtin_bit_cast(uint32_t, Z[t][q]);          \
+                    __asm__ volatile("" : "+v"(w_));                              \
+                    Z[t][q] = __builtin_bit_cast(f16x2, w_);                      \
+                }                                                                 \
+            }                                                                     \
+        }
+#define BGX_FOR_ELEM(BODY)                                                        \
+        BGX_LAUNDER_Z()                                                           \
+        _Pragma("unroll") for (int t = 0; t < kNT; ++t) {                         \
+            if (t < T || t == kVT) {                                              \
+                const int lt = lim - 32 * t - 4 * hh;                             \
+                const int at = act - 32 * t - 4 * hh;                             \
+                (void)at;                                                         \
+                _Pragma("unroll") for (int i = 0; i < 16; ++i) {                  \
+                    const int ko = (i & 3) + 8 * (i >> 2);                        \
+                    const float z = (float)Z[t][i >> 1][i & 1];                   \
+                    const float tz = ko < lt ? z * kL2e : -INFINITY;              \
+                    BODY                                                          \
+                }                                                                 \
+            }                                                                     \
+        }
+
+        float mx = -INFINITY;
+        BGX_FOR_ELEM(mx = fmaxf(mx, tz);)
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float se = 0.0f;
+        BGX_FOR_ELEM(se += __builtin_amdgcn_exp2f(tz - mx);)
+        se = hsum(se);
+        const float lse2 = mx + __log2f(se), nlse = -lse2 * kLn2;
+        float ent = 0.0f, entq = 0.0f, za = -INFINITY;
+        BGX_FOR_ELEM(const Elem e = elem(tz, lse2, nlse); ent = fmaf(-e.p, e.lp, ent); entq = fmaf(-e.p, e.q, entq);
+                     za = (ko == at && ko < lt) ? z : za;)
+        ent = hsum(ent);
+        entq = hsum(entq);
+        za = fmaxf(za, __shfl_xor(za, 32));
+        // per row (bgx_ppo_head_ex): ratio, clipped surrogate and their gradient
+        const float ua = za + nlse;                                   // -inf: act out of play
+        const float la = fminf(fmaxf(ua, kLogEps), kLog1mEps);
+        const float ina = la == ua ? 1.0f : 0.0f;
+        const float rt = __expf(la - olp);
+        const float s1 = rt * adv;
+        const float rc = fminf(fmaxf(rt, 1.0f - a.eps_clip), 1.0f + a.eps_clip);
+        const float s2 = rc * adv;
+        const float pol = -fminf(s1, s2);
+        const float w1 = s1 < s2 ? 1.0f : (s1 == s2 ? 0.5f : 0.0f);
+        const float w2 = (1.0f - w1) * ((rt >= 1.0f - a.eps_clip && rt <= 1.0f + a.eps_clip) ? 1.0f : 0.0f);
+        const float g_lp = -adv * rt * (w1 + w2) * ina;
+        const float gla = a.gscale * g_lp, k2 = fmaf(k1, entq, -gla);
+        const float dv = v - ret;
+        const float gv = a.gscale * a.c_value * 2.0f * dv;
+        if (valid && hh == 0) {
+            s_pol += pol;
+            s_val += dv * dv;
+            s_ent += ent;
+            a.stats[pos] = make_float4(lse2, k2, gla, gv);
+            a.info[pos] = (act & 0xFFFF) | (lim << 16);
+        }
+
+        // dz (fp16, [dlogits | dvalue | 0]), written over the tile's packed logits
+        BGX_LAUNDER_Z()
+        #pragma unroll
+        for (int t = 0; t < kNT; ++t) {
+            if (t < T || t == kVT) {
+                const int lt = lim - 32 * t - 4 * hh;
+                const int at = act - 32 * t - 4 * hh;
+                #pragma unroll
+                for (int i = 0; i < 16; i += 2) {
+                    float d2[2];
+                    #pragma unroll
+                    for (int e2 = 0; e2 < 2; ++e2) {
+                        const int ii = i + e2;
+                        const int ko = (ii & 3) + 8 * (ii >> 2);
+                        const float z = (float)Z[t][ii >> 1][ii & 1];
+                        const float tz = ko < lt ? z * kL2e : -INFINITY;
+                        const Elem e = elem(tz, lse2, nlse);
+                        float d = fmaf(e.p, fmaf(k1, e.q, k2), ko == at ? gla : 0.0f);
+                        if (t == kVT && ii == kVi) d = hh == kVh ? gv : d;
+                        d2[e2] = d;
+                    }
+                    Z[t][i >> 1] = f16x2{(_Float16)d2[0], (_Float16)d2[1]};
+                }
+                if (a.dy && valid) {
+                    _Float16* dyr = a.dy + (size_t)row * kAp + 32 * t + 4 * hh;
+                    #pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        *(uint2*)(dyr + 8 * q) = make_uint2(__builtin_bit_cast(uint32_t, Z[t][2 * q]),
+                                                            __builtin_bit_cast(uint32_t, Z[t][2 * q + 1]));
+                }
+            }
+        }
+        if (a.dy && valid && T < kVT) {             // the tiles skipped hold zeros
+            _Float16* dyr = a.dy + (size_t)row * kAp;
+            for (int c = 32 * T + 8 * hh; c < 32 * kVT; c += 16) *(uint4*)(dyr + c) = make_uint4(0, 0, 0, 0);
+        }
+        // dh^T = W2h^T dz^T per 32-unit hidden tile u: dz consumed unmoved as the B
+        // operand (registers 8s..8s+7 of tile t = k-step 2t + s), W2h^T from the LDS
+        // image by transposed reads; then fp16 rounding and ReLU's mask (h > 0).
+        // Register i = hidden 32u + (i&3) + 8(i>>2) + 4hh: 4 units per 8-byte store.
+        #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            f32x16 dacc;
+            #pragma unroll
+            for (int i = 0; i < 16; ++i) dacc[i] = 0.0f;
+            #pragma unroll
+            for (int t = 0; t < kNT; ++t) {
+                if (t < T || t == kVT) {
+                    const int ll = laundered_lane();
+                    #pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const f16x8 bfr = __builtin_bit_cast(
+                            f16x8, make_uint4(__builtin_bit_cast(uint32_t, Z[t][4 * s]), __builtin_bit_cast(uint32_t, Z[t][4 * s + 1]),
+                                              __builtin_bit_cast(uint32_t, Z[t][4 * s + 2]), __builtin_bit_cast(uint32_t, Z[t][4 * s + 3])));
+                        dacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(tr_operand(sw, 32 * t, s, u, ll), bfr, dacc, 0, 0, 0);
+                    }
+                    __asm__ volatile("" ::: "memory");
+                }
+            }
+            if (valid) {
+                _Float16* dhr = a.dh + (size_t)row * kH + 32 * u + 4 * hh;
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f16x4 o;
+                    #pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        o[e] = (hm[u] >> (8 * q + 4 * hh + e)) & 1u ? (_Float16)dacc[4 * q + e] : (_Float16)0.0f;
+                    *(f16x4*)(dhr + 8 * q) = o;
+                }
+            }
+        }
+    }
+#undef BGX_FOR_ELEM
+#undef BGX_LAUNDER_Z
+    // each lane of half 0 holds the fp32 sums of its own rows (a few dozen per lane);
+    // the wave and the workgroup add them in fp64
+    double dp = (double)s_pol, dvv = (double)s_val, de = (double)s_ent;
+    #pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        dp += __shfl_xor(dp, o);
+        dvv += __shfl_xor(dvv, o);
+        de += __shfl_xor(de, o);
+    }
+    if (l == 0) { red[wv][0] = dp; red[wv][1] = dvv; red[wv][2] = de; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        double t = 0.0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i][threadIdx.x];
+        atomicAdd(a.sums + threadIdx.x, t);
+    }
+}
+
+struct Gw2Args {
+    const _Float16* h;
+    const int32_t* perm;
+    const float4* stats;
+    const int32_t* info;
+    const _Float16* w2h;
+    const _Float16* b2h;
+    int m;
+    float k1;
+    const int32_t* plan;        // [0..16] task prefix per action tile, [17..32] first row tile per action tile
+    float* part;                // [task][kPart]
+};
+
+__global__ __launch_bounds__(256) void k_ppo_gw2(Gw2Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t sh[4][32 * 256];       // per-wave h tile, 8 KiB
+    __shared__ __attribute__((aligned(16))) float4 sst[4][32];
+    __shared__ int32_t sinf[4][32];
+    const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int r = l & 31, hh = l >> 5;
+    const int task = blockIdx.x * 4 + wv;
+    if (task >= a.plan[kNT]) return;                                        // whole waves only
+    int at = 0;
+    #pragma unroll
+    for (int b = 1; b < kNT; ++b) at = a.plan[b] <= task ? b : at;
+    const int ntiles = (a.m + 31) >> 5;
+    const int tile0 = a.plan[17 + at] + (task - a.plan[at]) * kTS;
+    const int tile1 = min(tile0 + kTS, ntiles);
+    uint4 bw[8];                                                            // B operand: W2h[32at + r][16s + 8hh + j]
+    const uint4* wp = (const uint4*)(a.w2h + (size_t)(32 * at + r) * kH);
+    #pragma unroll
+    for (int s = 0; s < 8; ++s) bw[s] = wp[2 * s + hh];
+    const float bias = (float)a.b2h[32 * at + r];
+    const int k = 32 * at + r;                                              // this lane's action column
+    f32x16 acc[4];
+    #pragma unroll
+    for (int u = 0; u < 4; ++u)
+        #pragma unroll
+        for (int i = 0; i < 16; ++i) acc[u][i] = 0.0f;
+    float gb = 0.0f;
+    uint8_t* img = sh[wv];
+    for (int tile = tile0; tile < tile1; ++tile) {
+        const int pos = tile * 32 + r;
+        const bool valid = pos < a.m;
+        const int row = a.perm[valid ? pos : a.m - 1];
+        const uint4* hp = (const uint4*)(a.h + (size_t)row * kH);
+        uint4 ha[8];                                                        // A operand: h[row][16s + 8hh + j]
+        #pragma unroll
+        for (int s = 0; s < 8; ++s) ha[s] = hp[2 * s + hh];
+        #pragma unroll
+        for (int s = 0; s < 8; ++s) *(uint4*)(img + swz(r, 2 * s + hh)) = ha[s];
+        if (hh == 0) {
+            sst[wv][r] = valid ? a.stats[pos] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            sinf[wv][r] = valid ? a.info[pos] : 0;                          // lim 0: nothing in play
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        f32x16 z;
+        #pragma unroll
+        for (int i = 0; i < 16; ++i) z[i] = 0.0f;
+        #pragma unroll
+        for (int s = 0; s < 8; ++s) z = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(ha[s]), as_h8(bw[s]), z, 0, 0, 0);
+        uint32_t D[8];
+        #pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+            float d2[2];
+            #pragma unroll
+            for (int e2 = 0; e2 < 2; ++e2) {
+                const int ii = i + e2;
+                const int ri = (ii & 3) + 8 * (ii >> 2) + 4 * hh;           // the register's row
+                const float4 st = sst[wv][ri];
+                const int inf = sinf[wv][ri];
+                const int lim = inf >> 16, act = inf & 0xFFFF;
+                const float zz = (float)(_Float16)(z[ii] + bias);
+                const float tz = k < lim ? zz * kL2e : -INFINITY;
+                const float nlse = -st.x * kLn2;
+                const Elem e = elem(tz, st.x, nlse);
+                float d = fmaf(e.p, fmaf(a.k1, e.q, st.y), k == act ? st.z : 0.0f);
+                if (k == kA) d = st.w;
+                const _Float16 dh16 = (_Float16)d;
+                gb += (float)dh16;
+                d2[e2] = (float)dh16;
+            }
+            D[i >> 1] = __builtin_bit_cast(uint32_t, f16x2{(_Float16)d2[0], (_Float16)d2[1]});
+        }
+        #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const f16x8 afr = __builtin_bit_cast(f16x8, make_uint4(D[4 * s], D[4 * s + 1], D[4 * s + 2], D[4 * s + 3]));
+            #pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afr, tr_operand(img, 0, s, u, l), acc[u], 0, 0, 0);
+        }
+        __builtin_amdgcn_wave_barrier();                                    // tile reads done before the next stores
+    }
+    gb = hsum(gb);
+    // C = gW2 tile: lane = hidden 32u + r, register i = action row (i&3) + 8(i>>2) + 4hh
+    float* out = a.part + (size_t)task * kPart;
+    #pragma unroll
+    for (int u = 0; u < 4; ++u)
+        #pragma unroll
+        for (int i = 0; i < 16; ++i) out[((i & 3) + 8 * (i >> 2) + 4 * hh) * kH + 32 * u + r] = acc[u][i];
+    if (hh == 0) out[32 * kH + r] = gb;
+}
+
+// gW2[32at + i][c] += sum over the action tile's tasks of their partials (fixed order)
+__global__ __launch_bounds__(256) void k_ppo_gw2_reduce(const float* __restrict__ part, const int32_t* __restrict__ plan,
+                                                        float* __restrict__ gw2, float* __restrict__ gb2) {
+    const int at = blockIdx.y;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kPart) return;
+    float s = 0.0f;
+    for (int t = plan[at]; t < plan[at + 1]; ++t) s += part[(size_t)t * kPart + e];
+    if (e < 32 * kH) gw2[(size_t)(32 * at) * kH + e] += s;
+    else gb2[32 * at + (e - 32 * kH)] += s;
+}
+
+}  // namespace
+
+extern int bgx_internal_fail(hipError_t e);
+
+extern "C" int bgx_ppo_rows(const void* h, const int32_t* perm, const uint8_t* records, const int32_t* actions,
+                            const float* old_logp, const float* returns, const float* adv, int32_t m, int32_t hidden,
+                            int32_t n_actions, const void* w2h, const void* b2h, float eps_clip, float c_value,
+                            float c_entropy, float grad_scale, void* dh, void* stats, int32_t* info, double* sums,
+                            void* dy, int32_t grid, void* stream) {
+    if (hidden != kH || n_actions != kA || m < 0) return BGX_EINVAL;
+    if (m == 0) return BGX_OK;
+    if (!h || !perm || !records || !actions || !old_logp || !returns || !adv || !w2h || !b2h || !dh || !stats ||
+        !info || !sums)
+        return BGX_EINVAL;
+    if (((uintptr_t)h | (uintptr_t)w2h | (uintptr_t)stats | (uintptr_t)dy) % 16 || ((uintptr_t)dh | (uintptr_t)b2h) % 8)
+        return BGX_EINVAL;
+    const int wgs = (m + 255) / 256;
+    const int g = grid > 0 ? grid : 256;
+    RowsArgs a{(const _Float16*)h, perm, records, actions, old_logp, returns, adv, (const _Float16*)w2h,
+               (const _Float16*)b2h, m, eps_clip, c_value, c_entropy, grad_scale, (_Float16*)dh, (float4*)stats,
+               info, sums, (_Float16*)dy};
+    hipLaunchKernelGGL(k_ppo_rows, dim3(wgs < g ? wgs : g), dim3(512), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
+extern "C" int64_t bgx_ppo_gw2_workspace(int32_t m) {
+    if (m < 0) return BGX_EINVAL;
+    const int64_t ntiles = (m + 31) / 32;
+    return (int64_t)kNT * ((ntiles + kTS - 1) / kTS) * kPart * (int64_t)sizeof(float);
+}
+
+extern "C" int bgx_ppo_gw2(const void* h, const int32_t* perm, const void* stats, const int32_t* info, int32_t m,
+                           int32_t hidden, int32_t n_actions, const void* w2h, const void* b2h, float k1,
+                           const int32_t* plan, float* workspace, float* gw2, float* gb2, void* stream) {
+    if (hidden != kH || n_actions != kA || m < 0) return BGX_EINVAL;
+    if (m == 0) return BGX_OK;
+    if (!h || !perm || !stats || !info || !w2h || !b2h || !plan || !workspace || !gw2 || !gb2) return BGX_EINVAL;
+    if (((uintptr_t)h | (uintptr_t)w2h | (uintptr_t)stats) % 16) return BGX_EINVAL;
+    const int ntiles = (m + 31) / 32;
+    const int max_tasks = kNT * ((ntiles + kTS - 1) / kTS);
+    Gw2Args a{(const _Float16*)h, perm, (const float4*)stats, info, (const _Float16*)w2h, (const _Float16*)b2h, m, k1,
+              plan, workspace};
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_ppo_gw2, dim3((max_tasks + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_ppo_gw2_reduce, dim3((kPart + 255) / 256, kNT), dim3(256), 0, s, workspace, plan, gw2, gb2);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}

@@ -12,7 +12,7 @@ HEADER = os.path.join(ROOT, "include", "bgx.h")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(bgx_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(bgx_\w+)\s*\(", txt, re.M)))
 
 
 def test_header_declares_api():

@@ -1,0 +1,145 @@
+"""The fused fp16 output layer + loss head (csrc/bg_ppo_fused.hip: bgx_ppo_rows,
+bgx_ppo_gw2) against the round-2 composition it replaces, on a real rollout:
+hipBLASLt logits y = h W2h^T + b2h, the loss-head kernel bgx_ppo_head_ex (pinned to
+torch autograd by test_gpu_train.py), dh = ReLU'(h) fp16(dy W2h), gW2 = dy^T h,
+gb2 = column sums of dy (ppo_agent.py:268-305 under autocast)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(seed=7, batch=4096, horizon=8):
+    from bgx.train import PPOTrainer, lane_returns
+    from bgx.ppo import global_normalize
+    tr = PPOTrainer(batch=batch, horizon=horizon, seed=seed)
+    tr.rollout()
+    b = tr.buf
+    R = global_normalize(lane_returns(b["rewards"], b["dones"]).reshape(-1)).contiguous()
+    adv = (R - b["values"].reshape(-1)).contiguous()
+    recs = b["records"].reshape(-1, 64).contiguous()
+    acts = b["actions"].reshape(-1).to(torch.int32).contiguous()
+    old = b["logp"].reshape(-1).contiguous()
+    net = tr.net
+    A, Hd = net.action_head.weight.shape
+    W2h = torch.zeros(512, Hd, dtype=torch.float16, device="cuda")
+    b2h = torch.zeros(512, dtype=torch.float16, device="cuda")
+    with torch.no_grad():
+        W2h[:A] = net.action_head.weight.half(); W2h[A] = net.value_head.weight[0].half()
+        b2h[:A] = net.action_head.bias.half(); b2h[A] = net.value_head.bias[0].half()
+        from bgx.engine import encode_records
+        h = torch.relu(F.linear(encode_records(recs, torch.float16), net.fc1.weight.half(), net.fc1.bias.half()))
+    return recs, acts, old, R, adv, W2h, b2h, h.contiguous()
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _fused(recs, acts, old, R, adv, W2h, b2h, h, coefs, perm, plan, want_dy=True):
+    from bgx import _lib
+    from bgx._lib import check
+    L = _lib.load()
+    m = recs.shape[0]
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    dh = torch.empty(m, 128, dtype=torch.float16, device="cuda")
+    stats = torch.empty(m, 4, dtype=torch.float32, device="cuda")
+    info = torch.empty(m, dtype=torch.int32, device="cuda")
+    sums = torch.zeros(3, dtype=torch.float64, device="cuda")
+    dy = torch.full((m, 512), float("nan"), dtype=torch.float16, device="cuda") if want_dy else None
+    eps, cv, ce, gs = coefs
+    check(L.bgx_ppo_rows(_p(h), _p(perm), _p(recs), _p(acts), _p(old), _p(R), _p(adv), m, 128, 500, _p(W2h), _p(b2h),
+                         eps, cv, ce, gs, _p(dh), _p(stats), _p(info), _p(sums), _p(dy), 0, s), "bgx_ppo_rows")
+    gw2 = torch.zeros(512, 128, dtype=torch.float32, device="cuda")
+    gb2 = torch.zeros(512, dtype=torch.float32, device="cuda")
+    ws = torch.empty(L.bgx_ppo_gw2_workspace(m) // 4, dtype=torch.float32, device="cuda")
+    k1 = float(np.float32(gs) * np.float32(ce))
+    check(L.bgx_ppo_gw2(_p(h), _p(perm), _p(stats), _p(info), m, 128, 500, _p(W2h), _p(b2h), k1, _p(plan), _p(ws),
+                        _p(gw2), _p(gb2), s), "bgx_ppo_gw2")
+    torch.cuda.synchronize()
+    return dh, dy, gw2, gb2, sums
+
+
+def _reference(recs, acts, old, R, adv, W2h, b2h, h, coefs):
+    from bgx import _lib
+    from bgx._lib import check
+    L = _lib.load()
+    m = recs.shape[0]
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    y = F.linear(h, W2h, b2h).contiguous()
+    vals = y[:, 500].contiguous()
+    dy = torch.empty_like(y)
+    dval = torch.empty_like(vals)
+    sums = torch.zeros(3, dtype=torch.float64, device="cuda")
+    colsum = torch.empty(2048, 512, dtype=torch.float32, device="cuda")
+    eps, cv, ce, gs = coefs
+    check(L.bgx_ppo_head_ex(_p(y), 1, 512, _p(vals), _p(recs), _p(acts), _p(old), _p(R), _p(adv), m, 500, eps, cv, ce,
+                            gs, _p(dy), 512, _p(dval), _p(sums), 1, _p(colsum), s), "bgx_ppo_head_ex")
+    dh = (dy @ W2h) * (h > 0)
+    gw2 = dy.float().t() @ h.float()
+    gb2 = dy.float().sum(0)
+    torch.cuda.synchronize()
+    return dh, dy, gw2, gb2, sums
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm())
+
+
+COEFS = (0.25, 0.5, 0.15, 16.0)      # eps_clip, value coef, entropy coef, per-row gradient scale
+
+
+def test_fused_head_matches_round2_composition():
+    from bgx.train import ppo_row_plan
+    args = _setup()
+    recs = args[0]
+    perm, plan = ppo_row_plan(recs)
+    dh, dy, gw2, gb2, sums = _fused(*args, COEFS, perm, plan)
+    rdh, rdy, rgw2, rgb2, rsums = _reference(*args, COEFS)
+    # loss sums: the same per-row formulas; fp32 log-sum-exp in another order
+    m = recs.shape[0]
+    assert torch.allclose(sums / m, rsums / m, rtol=1e-5, atol=1e-6), (sums / m, rsums / m)
+    # dy: fp16 values of the same formulas (logits from MFMA vs hipBLASLt: an fp16
+    # logit may differ by one ulp where the fp32 sums round differently)
+    assert not torch.isnan(dy).any()
+    d = (dy.float() - rdy.float()).abs()
+    tol = rdy.float().abs() * 2e-3 + 1e-6
+    assert float((d > tol).float().mean()) < 1e-3, float((d > tol).float().mean())
+    assert _rel(dy, rdy) < 2e-3
+    assert _rel(dh, rdh) < 2e-3
+    assert _rel(gw2, rgw2) < 2e-3 and _rel(gb2, rgb2) < 2e-3
+    # gW2 / gb2 from the recomputed dz == dy^T h of the rows kernel's own dy
+    h = args[-1]
+    assert _rel(gw2, dy.float().t() @ h.float()) < 1e-5
+    assert _rel(gb2, dy.float().sum(0)) < 1e-5
+    # masked columns (past the legal count of a row with legal moves) get exactly 0
+    cnt = recs[:, 60].int() | (recs[:, 61].int() << 8)
+    cols = torch.arange(500, device="cuda")[None, :]
+    masked = (cols >= cnt[:, None]) & (cnt[:, None] > 0)
+    assert bool((dy[:, :500][masked] == 0).all())
+    assert bool((dy[:, 501:] == 0).all())
+
+
+def test_fused_head_row_order_invariant():
+    """Any row order gives the same dy / dh (per-row work) and the same gW2 up to
+    the fp32 summation order: the sort only schedules."""
+    from bgx.train import ppo_row_plan
+    args = _setup(seed=3, batch=2048, horizon=5)
+    recs = args[0]
+    m = recs.shape[0]
+    perm, plan = ppo_row_plan(recs)
+    a = _fused(*args, COEFS, perm, plan)
+    ident = torch.arange(m, dtype=torch.int32, device="cuda")
+    ntiles = (m + 31) // 32
+    tasks = (ntiles + 31) // 32
+    plan2 = torch.tensor([tasks * i for i in range(17)] + [0] * 16, dtype=torch.int32, device="cuda")
+    rev = torch.flip(ident, [0]).contiguous()
+    for p2 in (ident, rev):
+        b = _fused(*args, COEFS, p2, plan2)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        assert _rel(b[2], a[2]) < 1e-6 and _rel(b[3], a[3]) < 1e-6
+        assert torch.allclose(a[4] / m, b[4] / m, rtol=1e-6, atol=1e-7)
