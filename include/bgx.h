@@ -259,12 +259,17 @@ int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_de
  * value_head.weight; 0] and b2h [512] fp16 likewise; h [m][128] fp16 = the fc1
  * output (bgx_fc1_records).  perm [m] lists the rows in ascending order of the
  * number of 32-action tiles they need (ceil(cnt / 32), 16 for cnt = 0; any order
- * is correct, sorted is fast).
+ * is correct, sorted is fast); perm = NULL: the rows are already in that order
+ * (PPOTrainer gathers them so once per update, and every kernel reads them
+ * contiguously).
  * bgx_ppo_rows: per row the loss parts (added to sums[0..2] as bgx_ppo_head),
  * dh [m][128] fp16 = ReLU'(h) * fp16(dy W2h) (original row order), and the row
  * statistics stats [m] (16 B, 16-byte aligned) + info [m] (int32) in perm order
  * for bgx_ppo_gw2; dy_or_null [m][512] fp16 receives dy = [dlogits | dvalue | 0]
- * (tests).  grid <= 0: 256 workgroups.
+ * (tests).  row_plan int32[8] = the row tiles (of perm order) [lo, hi) handled by
+ * the variants for at most 1, 2, 4 and 16 leading action tiles (every row tile in
+ * exactly one range; a tile's count is the largest of its rows').  grid <= 0:
+ * persistent grids of 4 workgroups per CU (1 for the 16-tile variant).
  * bgx_ppo_gw2: gw2 [512][128] += dy^T h and gb2 [512] += column sums of dy (fp32),
  * dy recomputed from the statistics; plan int32[33] = task prefix per action tile
  * (17 entries, tasks of BGX_PPO_GW2_TASK_TILES row tiles) then the first row tile
@@ -275,7 +280,7 @@ int bgx_ppo_rows(const void* h_dev, const int32_t* perm_dev, const uint8_t* reco
                  const float* old_logp_dev, const float* returns_dev, const float* adv_dev, int32_t m, int32_t hidden,
                  int32_t n_actions, const void* w2h_dev, const void* b2h_dev, float eps_clip, float c_value,
                  float c_entropy, float grad_scale, void* dh_dev, void* stats_dev, int32_t* info_dev,
-                 double* sums_dev, void* dy_or_null, int32_t grid, void* stream);
+                 double* sums_dev, void* dy_or_null, const int32_t* row_plan_dev, int32_t grid, void* stream);
 int64_t bgx_ppo_gw2_workspace(int32_t m);
 int bgx_ppo_gw2(const void* h_dev, const int32_t* perm_dev, const void* stats_dev, const int32_t* info_dev, int32_t m,
                 int32_t hidden, int32_t n_actions, const void* w2h_dev, const void* b2h_dev, float k1,

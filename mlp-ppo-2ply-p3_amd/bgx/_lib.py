@@ -59,7 +59,7 @@ SIGNATURES = {
     "bgx_fc1_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
     "bgx_fc1_records": (ctypes.c_int, [_P, _I32, _P, _P, _I32, _P, _P]),
     "bgx_ppo_rows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, ctypes.c_float,
-                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _I32, _P]),
+                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _I32, _P]),
     "bgx_ppo_gw2_workspace": (ctypes.c_int64, [_I32]),
     "bgx_ppo_gw2": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),

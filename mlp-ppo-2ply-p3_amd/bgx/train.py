@@ -341,7 +341,9 @@ def ppo_row_plan(records: torch.Tensor, n_actions: int = 500):
     (ceil(cnt / 32); all 16 when cnt = 0, every action then being masked by the
     same constant); rows are sorted by that count (stable).  plan = the k_ppo_gw2
     task prefix per action tile (17) and the first row tile (in sorted order) that
-    reaches each action tile (16).  Device tensors only: no host sync."""
+    reaches each action tile (16); row_plan = the row tiles [lo, hi) of the
+    bgx_ppo_rows variants for at most 1, 2, 4 and 16 leading action tiles.  Device
+    tensors only: no host sync."""
     m = records.shape[0]
     cnt = records[:, 60].to(torch.int32) | (records[:, 61].to(torch.int32) << 8)
     lim = torch.where(cnt == 0, torch.full_like(cnt, n_actions), cnt.clamp(max=n_actions))
@@ -353,7 +355,12 @@ def ppo_row_plan(records: torch.Tensor, n_actions: int = 500):
     ntiles = (m + 31) // 32
     tasks = (ntiles - start + PPO_GW2_TASK_TILES - 1) // PPO_GW2_TASK_TILES
     pre = torch.cat([torch.zeros(1, dtype=tasks.dtype, device=tasks.device), torch.cumsum(tasks, 0)])
-    return perm, torch.cat([pre, start]).to(torch.int32).contiguous()
+    # row tiles whose last (largest) row needs <= k tiles: cum[k] // 32, all of them at cum[k] == m
+    e = torch.where(cum[[1, 2, 4]] >= m, torch.full_like(cum[[1, 2, 4]], ntiles), cum[[1, 2, 4]] // 32)
+    z = torch.zeros(1, dtype=e.dtype, device=e.device)
+    nt = torch.full_like(z, ntiles)
+    row_plan = torch.stack([z[0], e[0], e[0], e[1], e[1], e[2], e[2], nt[0]]).to(torch.int32).contiguous()
+    return perm, torch.cat([pre, start]).to(torch.int32).contiguous(), row_plan
 
 
 def _fused_head_ok(net) -> bool:
@@ -402,7 +409,7 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
                 x = torch.zeros(m, 208, dtype=torch.float16, device=dev)
                 x[:, :F_in] = feats[:, :F_in]
                 x[:, FEAT_BIAS_COL] = 1.0
-            perm, plan = prep["plan"] if "plan" in prep else ppo_row_plan(rec, A)
+            perm, plan, row_plan = prep["plan"] if "plan" in prep else ppo_row_plan(rec, A)
             h = torch.empty(m, Hd, dtype=torch.float16, device=dev)
             check(L.bgx_fc1_records(p(rec), m, p(w1pack), p(b1h), Hd, p(h), stream), "bgx_fc1_records")
             dh = torch.empty(m, Hd, dtype=torch.float16, device=dev)
@@ -410,11 +417,13 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
             info = torch.empty(m, dtype=torch.int32, device=dev)
             acts = actions.to(torch.int32).contiguous()
             old, ret, ad = old_logp.float().contiguous(), returns.float().contiguous(), adv.float().contiguous()
-            check(L.bgx_ppo_rows(p(h), p(perm), p(rec), p(acts), p(old), p(ret), p(ad), m, Hd, A, p(W2h), p(b2h),
-                                 eps, c_v, c_e, row_scale, p(dh), p(stats), p(info), p(sums), None, 0, stream),
+            pp = None if perm is None else p(perm)             # None: rows already in plan order
+            check(L.bgx_ppo_rows(p(h), pp, p(rec), p(acts), p(old), p(ret), p(ad), m, Hd, A, p(W2h), p(b2h),
+                                 eps, c_v, c_e, row_scale, p(dh), p(stats), p(info), p(sums), None, p(row_plan), 0,
+                                 stream),
                   "bgx_ppo_rows")
             ws = torch.empty(L.bgx_ppo_gw2_workspace(m) // 4, dtype=torch.float32, device=dev)
-            check(L.bgx_ppo_gw2(p(h), p(perm), p(stats), p(info), m, Hd, A, p(W2h), p(b2h), k1, p(plan), p(ws),
+            check(L.bgx_ppo_gw2(p(h), pp, p(stats), p(info), m, Hd, A, p(W2h), p(b2h), k1, p(plan), p(ws),
                                 p(gW2), p(gb2), stream), "bgx_ppo_gw2")
             gW1 += _wgrad(dh, x)
         if post != 1.0:
@@ -566,14 +575,28 @@ class PPOTrainer:
                                 width=208 if fused_head else (FEAT_W if manual else 198))
                  for s in range(0, N, self.chunk)] if self.fused else None
         preps = [{} for _ in range(0, N, self.chunk)]
-        if fused_head:      # the ones column (fc1's bias gradient) and the row plan, once per update
+        sorted_rows = [None for _ in range(0, N, self.chunk)]
+        if fused_head:
+            # once per update: each chunk's rows in the order of the fused head's row plan
+            # (by the number of action tiles a row needs), gathered so that every kernel
+            # of the 4 epochs reads them contiguously; the ones column (fc1's bias gradient)
             for i, s in enumerate(range(0, N, self.chunk)):
+                e = min(N, s + self.chunk)
+                perm, plan, row_plan = ppo_row_plan(recs[s:e], self.A)
+                pl = perm.long()
+                sorted_rows[i] = (recs[s:e][pl].contiguous(), acts[s:e][pl].contiguous(), old[s:e][pl].contiguous(),
+                                  R[s:e][pl].contiguous(), adv[s:e][pl].contiguous())
+                feats[i] = encode_records(sorted_rows[i][0], torch.float16, width=208)
                 feats[i][:, FEAT_BIAS_COL] = 1.0
-                preps[i] = {"bias_col": True, "plan": ppo_row_plan(recs[s:min(N, s + self.chunk)], self.A)}
+                preps[i] = {"bias_col": True, "plan": (None, plan, row_plan)}
 
         def chunks():
             for i, s in enumerate(range(0, N, self.chunk)):
                 e = min(N, s + self.chunk)
+                if sorted_rows[i] is not None:
+                    rr, aa, oo, RR, dd = sorted_rows[i]
+                    yield feats[i], None, aa, oo, RR, dd, rr, preps[i]
+                    continue
                 if self.fused:      # the loss kernel reads the legal counts from the records
                     f, legal = feats[i], None
                 else:

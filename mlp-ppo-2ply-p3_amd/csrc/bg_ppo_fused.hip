@@ -21,7 +21,7 @@
 //    action), dz recomputed from the row statistics (bit-identical formulas),
 //    and dz^T h accumulated over the wave's rows (h^T from a per-wave LDS tile
 //    via ds_read_b64_tr_b16); the bias gradient gb2 is the row sum of dz in the
-//    lane.  Per-task partials are summed by k_ppo_gw2_reduce (deterministic).
+//    lane.  Per-task partials are summed by k_ppo_gw2_sum1/2 (fixed order).
 //
 // Sparsity (exact): a row with cnt >= 1 legal actions has masked logits at
 // z + log(1e-45) (ppo_agent.py:166), i.e. probabilities below 1e-44 relative:
@@ -138,45 +138,93 @@ struct RowsArgs {
     _Float16* dy;               // optional [m][512] dL/dy (tests), original row order
 };
 
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_ppo_rows(RowsArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t sw[kAp * 256];     // W2h, 128 KiB
-    __shared__ __attribute__((aligned(16))) float sb[kAp];
-    __shared__ double red[8][3];
-    for (int i = threadIdx.x; i < kAp * 16; i += blockDim.x)
-        *(uint4*)(sw + swz(i >> 4, i & 15)) = ((const uint4*)a.w2h)[i];
-    for (int i = threadIdx.x; i < kAp; i += blockDim.x) sb[i] = (float)a.b2h[i];
+// One variant per bound TM on the leading action tiles a row tile needs (TM = 1, 2, 4,
+// 16): the used W2h tiles sit in LDS (tile t < TM at image tile t, the value tile at
+// image tile TM), the packed logits take 8 registers per used tile, and the small
+// variants keep 4 waves per workgroup with the next row tile's inputs loaded behind the
+// current one's work.  Each variant walks the row tiles [range[0], range[1]) of the
+// sorted order.
+template <int TM>
+struct RowsCfg {
+    static constexpr int kImg = TM < kNT ? TM + 1 : kNT;        // W2h tiles in LDS
+    static constexpr int kWaves = TM < kNT ? 4 : 8;              // waves per workgroup
+    static constexpr bool kPrefetch = false;
+};
+
+struct RowIn {
+    int row, cnt, act;
+    float adv, olp, ret;
+    uint4 hf[8];                                                 // B operand: h[row][16s + 8hh + j]
+};
+
+__device__ __forceinline__ void load_row(const RowsArgs& a, int tile, RowIn& in) {
+    const int l = threadIdx.x & 63;
+    const int pos = tile * 32 + (l & 31);
+    const int p = pos < a.m ? pos : a.m - 1;
+    in.row = a.perm ? a.perm[p] : p;
+    const uint8_t* rec = a.recs + (size_t)in.row * 64;
+    in.cnt = (int)rec[60] | ((int)rec[61] << 8);
+    in.act = a.act[in.row];
+    in.adv = a.adv[in.row];
+    in.olp = a.old_logp[in.row];
+    in.ret = a.ret[in.row];
+    const uint4* hp = (const uint4*)(a.h + (size_t)in.row * kH);
+    #pragma unroll
+    for (int s = 0; s < 8; ++s) in.hf[s] = hp[2 * s + (l >> 5)];
+}
+
+template <int TM>
+__global__ __launch_bounds__(TM < kNT ? 256 : 512) __attribute__((amdgpu_waves_per_eu(TM == 1 ? 2 : (TM == 2 ? 2 : 2))))
+void k_ppo_rows(RowsArgs a, const int32_t* __restrict__ range) {
+    using C = RowsCfg<TM>;
+    constexpr int kW = C::kWaves;
+    __shared__ __attribute__((aligned(16))) uint8_t sw[C::kImg * 32 * 256];
+    __shared__ __attribute__((aligned(16))) float sb[C::kImg * 32];
+    __shared__ double red[kW][3];
+    const int lo = range[0], hi = range[1];
+    if (lo + (int)blockIdx.x * kW >= hi) return;                  // whole workgroups only
+    for (int i = threadIdx.x; i < C::kImg * 32 * 16; i += blockDim.x) {
+        const int irow = i >> 4, it = irow >> 5;
+        const int srow = 32 * (it < TM ? it : kVT) + (irow & 31);
+        *(uint4*)(sw + swz(irow, i & 15)) = ((const uint4*)a.w2h)[srow * 16 + (i & 15)];
+    }
+    for (int i = threadIdx.x; i < C::kImg * 32; i += blockDim.x)
+        sb[i] = (float)a.b2h[32 * ((i >> 5) < TM ? (i >> 5) : kVT) + (i & 31)];
     __syncthreads();
 
     const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = l & 31, hh = l >> 5;
-    const int ntiles = (a.m + 31) >> 5;
     const float k1 = a.gscale * a.c_entropy;
     float s_pol = 0.0f, s_val = 0.0f, s_ent = 0.0f;
-    for (int tile = blockIdx.x * 8 + wv; tile < ntiles; tile += gridDim.x * 8) {
+    const int stride = gridDim.x * kW;
+    int tile = lo + blockIdx.x * kW + wv;
+    RowIn cur;
+    if (C::kPrefetch && tile < hi) load_row(a, tile, cur);
+    for (; tile < hi; tile += stride) {
+        RowIn nxt;
+        if (C::kPrefetch) {
+            if (tile + stride < hi) load_row(a, tile + stride, nxt);
+        } else {
+            load_row(a, tile, cur);
+        }
         const int pos = tile * 32 + r;
         const bool valid = pos < a.m;
-        const int row = a.perm[valid ? pos : a.m - 1];
-        const uint8_t* rec = a.recs + (size_t)row * 64;
-        const int cnt = (int)rec[60] | ((int)rec[61] << 8);
-        const int lim = cnt == 0 ? kA : (cnt < kA ? cnt : kA);   // columns [0, lim) in play
-        const int act = a.act[row];
-        const float adv = a.adv[row], olp = a.old_logp[row], ret = a.ret[row];
-        int T = (lim + 31) >> 5;                                  // action tiles this row needs
+        const int row = cur.row, act = cur.act;
+        const int lim = cur.cnt == 0 ? kA : (cur.cnt < kA ? cur.cnt : kA);   // columns [0, lim) in play
+        // leading action tiles this row needs; T = the wave's largest (1..16), by a binary
+        // search over ballots (no lane shuffles to keep addresses for)
+        const int tr = (lim + 31) >> 5;
+        int T = 0;
         #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) T = max(T, __shfl_xor(T, o));
-        T = __builtin_amdgcn_readfirstlane(T);
+        for (int b = 16; b >= 1; b >>= 1) T += __ballot(tr >= T + b) ? b : 0;
 
-        uint4 hf[8];                                              // B operand: h[row][16s + 8hh + j]
-        const uint4* hp = (const uint4*)(a.h + (size_t)row * kH);
-        #pragma unroll
-        for (int s = 0; s < 8; ++s) hf[s] = hp[2 * s + hh];
         uint32_t hm[4];                                           // bit k: h[row][32u + k] > 0
         #pragma unroll
         for (int u = 0; u < 4; ++u) {
             uint32_t own = 0;
             #pragma unroll
             for (int half = 0; half < 2; ++half) {
-                const uint4 w = hf[2 * u + half];
+                const uint4 w = cur.hf[2 * u + half];
                 const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
                 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -187,11 +235,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             hm[u] = own | (uint32_t)__shfl_xor((int)own, 32);
         }
 
-        // Z^T tiles (lane = row; register i = action 32t + (i&3) + 8(i>>2) + 4hh), fp16
-        f16x2 Z[kNT][8];
+        // Z^T tiles (lane = row; register i = action 32t + (i&3) + 8(i>>2) + 4hh); image
+        // tile k holds action tile t = k < TM ? k : kVT.  The logits are fp16 (autocast's
+        // GEMM output).  Small variants keep tz = z log2(e) (or -inf out of play) in fp32
+        // registers; the 16-tile one keeps the packed fp16 logits and re-derives tz per pass.
+        constexpr bool kKeep = TM < kNT;
+        f16x2 Z[kKeep ? 1 : C::kImg][8];
+        float TZ[kKeep ? C::kImg : 1][16];
+        float v_own = 0.0f;
+#define BGX_TILE_ON(k) (((k) < TM && (k) != kVT) ? (k) < T : true)
+#define BGX_TILE_T(k) ((k) < TM ? (k) : kVT)
+        constexpr int kVk = C::kImg - 1;                          // image tile of the value column
         #pragma unroll
-        for (int t = 0; t < kNT; ++t) {
-            if (t < T || t == kVT) {
+        for (int k = 0; k < C::kImg; ++k) {
+            if (BGX_TILE_ON(k)) {
                 f32x16 acc;
                 #pragma unroll
                 for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
@@ -199,41 +256,54 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
                 #pragma unroll
                 for (int s = 0; s < 8; ++s)
                     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(
-                        as_h8(*(const uint4*)(sw + swz(32 * t + (ll & 31), 2 * s + (ll >> 5)))), as_h8(hf[s]), acc, 0, 0, 0);
+                        as_h8(*(const uint4*)(sw + swz(32 * k + (ll & 31), 2 * s + (ll >> 5)))), as_h8(cur.hf[s]), acc,
+                        0, 0, 0);
+                const int lt = lim - 32 * BGX_TILE_T(k) - 4 * hh;
                 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const float4 bb = *(const float4*)(sb + 32 * t + 8 * q + 4 * hh);
-                    Z[t][2 * q] = f16x2{(_Float16)(acc[4 * q] + bb.x), (_Float16)(acc[4 * q + 1] + bb.y)};
-                    Z[t][2 * q + 1] = f16x2{(_Float16)(acc[4 * q + 2] + bb.z), (_Float16)(acc[4 * q + 3] + bb.w)};
+                    const float4 bb = *(const float4*)(sb + 32 * k + 8 * q + 4 * hh);
+                    const float bq[4] = {bb.x, bb.y, bb.z, bb.w};
+                    #pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int i = 4 * q + e;
+                        const _Float16 zh = (_Float16)(acc[i] + bq[e]);
+                        if (k == kVk && i == kVi) v_own = (float)zh;
+                        if (kKeep) {
+                            const int ko = (i & 3) + 8 * (i >> 2);
+                            TZ[kKeep ? k : 0][i] = ko < lt ? (float)zh * kL2e : -INFINITY;
+                        } else {
+                            Z[kKeep ? 0 : k][i >> 1][i & 1] = zh;
+                        }
+                    }
                 }
                 __asm__ volatile("" ::: "memory");       // one tile's LDS reads in flight at a time
             }
         }
-        const float v = __shfl((float)Z[kVT][kVi >> 1][kVi & 1], r + 32 * kVh);
+        const float v = __shfl(v_own, r + 32 * kVh);
 
-// Each pass re-reads the packed fp16 logits: laundering them first keeps LLVM from
-// keeping the fp32 conversions (256 per lane) alive across passes.
+// Each pass of the 16-tile variant re-reads the packed fp16 logits: laundering them
+// first keeps LLVM from keeping the fp32 conversions alive across passes.
 #define BGX_LAUNDER_Z()                                                           \
-        _Pragma("unroll") for (int t = 0; t < kNT; ++t) {                         \
-            if (t < T || t == kVT) {                                              \
+        _Pragma("unroll") for (int k = 0; k < C::kImg; ++k) {                     \
+            if (!kKeep && BGX_TILE_ON(k)) {                                       \
                 _Pragma("unroll") for (int q = 0; q < 8; ++q) {                   \
-                    uint32_t w_ = __builtin_bit_cast(uint32_t, Z[t][q]);          \
+                    uint32_t w_ = __builtin_bit_cast(uint32_t, Z[kKeep ? 0 : k][q]); \
                     __asm__ volatile("" : "+v"(w_));                              \
-                    Z[t][q] = __builtin_bit_cast(f16x2, w_);                      \
+                    Z[kKeep ? 0 : k][q] = __builtin_bit_cast(f16x2, w_);          \
                 }                                                                 \
             }                                                                     \
         }
 #define BGX_FOR_ELEM(BODY)                                                        \
         BGX_LAUNDER_Z()                                                           \
-        _Pragma("unroll") for (int t = 0; t < kNT; ++t) {                         \
-            if (t < T || t == kVT) {                                              \
-                const int lt = lim - 32 * t - 4 * hh;                             \
-                const int at = act - 32 * t - 4 * hh;                             \
+        _Pragma("unroll") for (int k = 0; k < C::kImg; ++k) {                     \
+            if (BGX_TILE_ON(k)) {                                                 \
+                const int lt = lim - 32 * BGX_TILE_T(k) - 4 * hh;                 \
+                const int at = act - 32 * BGX_TILE_T(k) - 4 * hh;                 \
                 (void)at;                                                         \
                 _Pragma("unroll") for (int i = 0; i < 16; ++i) {                  \
                     const int ko = (i & 3) + 8 * (i >> 2);                        \
-                    const float z = (float)Z[t][i >> 1][i & 1];                   \
-                    const float tz = ko < lt ? z * kL2e : -INFINITY;              \
+                    const float tz = kKeep ? TZ[kKeep ? k : 0][i]                 \
+                        : (ko < lt ? (float)Z[kKeep ? 0 : k][i >> 1][i & 1] * kL2e : -INFINITY); \
                     BODY                                                          \
                 }                                                                 \
             }                                                                     \
@@ -246,14 +316,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         BGX_FOR_ELEM(se += __builtin_amdgcn_exp2f(tz - mx);)
         se = hsum(se);
         const float lse2 = mx + __log2f(se), nlse = -lse2 * kLn2;
-        float ent = 0.0f, entq = 0.0f, za = -INFINITY;
+        float ent = 0.0f, entq = 0.0f, ua = -INFINITY;
         BGX_FOR_ELEM(const Elem e = elem(tz, lse2, nlse); ent = fmaf(-e.p, e.lp, ent); entq = fmaf(-e.p, e.q, entq);
-                     za = (ko == at && ko < lt) ? z : za;)
+                     ua = ko == at ? e.u : ua;)
         ent = hsum(ent);
         entq = hsum(entq);
-        za = fmaxf(za, __shfl_xor(za, 32));
+        ua = fmaxf(ua, __shfl_xor(ua, 32));                           // -inf: act out of play
         // per row (bgx_ppo_head_ex): ratio, clipped surrogate and their gradient
-        const float ua = za + nlse;                                   // -inf: act out of play
+        const float adv = cur.adv, olp = cur.olp, ret = cur.ret;
         const float la = fminf(fmaxf(ua, kLogEps), kLog1mEps);
         const float ina = la == ua ? 1.0f : 0.0f;
         const float rt = __expf(la - olp);
@@ -275,11 +345,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             a.info[pos] = (act & 0xFFFF) | (lim << 16);
         }
 
-        // dz (fp16, [dlogits | dvalue | 0]), written over the tile's packed logits
+        // dz (fp16, [dlogits | dvalue | 0]); the 16-tile variant writes it over its logits
+        f16x2 Dz[kKeep ? C::kImg : 1][8];
+#define BGX_DZ(k) (kKeep ? Dz[kKeep ? (k) : 0] : Z[kKeep ? 0 : (k)])
         BGX_LAUNDER_Z()
         #pragma unroll
-        for (int t = 0; t < kNT; ++t) {
-            if (t < T || t == kVT) {
+        for (int k = 0; k < C::kImg; ++k) {
+            if (BGX_TILE_ON(k)) {
+                const int t = BGX_TILE_T(k);
                 const int lt = lim - 32 * t - 4 * hh;
                 const int at = act - 32 * t - 4 * hh;
                 #pragma unroll
@@ -289,30 +362,31 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
                     for (int e2 = 0; e2 < 2; ++e2) {
                         const int ii = i + e2;
                         const int ko = (ii & 3) + 8 * (ii >> 2);
-                        const float z = (float)Z[t][ii >> 1][ii & 1];
-                        const float tz = ko < lt ? z * kL2e : -INFINITY;
+                        const float tz = kKeep ? TZ[kKeep ? k : 0][ii]
+                            : (ko < lt ? (float)Z[kKeep ? 0 : k][ii >> 1][ii & 1] * kL2e : -INFINITY);
                         const Elem e = elem(tz, lse2, nlse);
                         float d = fmaf(e.p, fmaf(k1, e.q, k2), ko == at ? gla : 0.0f);
-                        if (t == kVT && ii == kVi) d = hh == kVh ? gv : d;
+                        if (k == kVk && ii == kVi) d = hh == kVh ? gv : d;
                         d2[e2] = d;
                     }
-                    Z[t][i >> 1] = f16x2{(_Float16)d2[0], (_Float16)d2[1]};
+                    BGX_DZ(k)[i >> 1] = f16x2{(_Float16)d2[0], (_Float16)d2[1]};
                 }
                 if (a.dy && valid) {
                     _Float16* dyr = a.dy + (size_t)row * kAp + 32 * t + 4 * hh;
                     #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        *(uint2*)(dyr + 8 * q) = make_uint2(__builtin_bit_cast(uint32_t, Z[t][2 * q]),
-                                                            __builtin_bit_cast(uint32_t, Z[t][2 * q + 1]));
+                        *(uint2*)(dyr + 8 * q) = make_uint2(__builtin_bit_cast(uint32_t, BGX_DZ(k)[2 * q]),
+                                                            __builtin_bit_cast(uint32_t, BGX_DZ(k)[2 * q + 1]));
                 }
             }
         }
-        if (a.dy && valid && T < kVT) {             // the tiles skipped hold zeros
+        if (a.dy && valid) {                         // the action tiles skipped hold zeros
+            const int t0 = T < TM ? T : TM;
             _Float16* dyr = a.dy + (size_t)row * kAp;
-            for (int c = 32 * T + 8 * hh; c < 32 * kVT; c += 16) *(uint4*)(dyr + c) = make_uint4(0, 0, 0, 0);
+            for (int c = 32 * t0 + 8 * hh; c < 32 * kVT; c += 16) *(uint4*)(dyr + c) = make_uint4(0, 0, 0, 0);
         }
         // dh^T = W2h^T dz^T per 32-unit hidden tile u: dz consumed unmoved as the B
-        // operand (registers 8s..8s+7 of tile t = k-step 2t + s), W2h^T from the LDS
+        // operand (registers 8s..8s+7 of a tile = its k-step s), W2h^T from the LDS
         // image by transposed reads; then fp16 rounding and ReLU's mask (h > 0).
         // Register i = hidden 32u + (i&3) + 8(i>>2) + 4hh: 4 units per 8-byte store.
         #pragma unroll
@@ -321,15 +395,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
             #pragma unroll
             for (int i = 0; i < 16; ++i) dacc[i] = 0.0f;
             #pragma unroll
-            for (int t = 0; t < kNT; ++t) {
-                if (t < T || t == kVT) {
+            for (int k = 0; k < C::kImg; ++k) {
+                if (BGX_TILE_ON(k)) {
                     const int ll = laundered_lane();
                     #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const f16x8 bfr = __builtin_bit_cast(
-                            f16x8, make_uint4(__builtin_bit_cast(uint32_t, Z[t][4 * s]), __builtin_bit_cast(uint32_t, Z[t][4 * s + 1]),
-                                              __builtin_bit_cast(uint32_t, Z[t][4 * s + 2]), __builtin_bit_cast(uint32_t, Z[t][4 * s + 3])));
-                        dacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(tr_operand(sw, 32 * t, s, u, ll), bfr, dacc, 0, 0, 0);
+                            f16x8, make_uint4(__builtin_bit_cast(uint32_t, BGX_DZ(k)[4 * s]),
+                                              __builtin_bit_cast(uint32_t, BGX_DZ(k)[4 * s + 1]),
+                                              __builtin_bit_cast(uint32_t, BGX_DZ(k)[4 * s + 2]),
+                                              __builtin_bit_cast(uint32_t, BGX_DZ(k)[4 * s + 3])));
+                        dacc = __builtin_amdgcn_mfma_f32_32x32x16_f16(tr_operand(sw, 32 * k, s, u, ll), bfr, dacc,
+                                                                      0, 0, 0);
                     }
                     __asm__ volatile("" ::: "memory");
                 }
@@ -346,9 +423,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
                 }
             }
         }
+        if (C::kPrefetch) cur = nxt;
     }
 #undef BGX_FOR_ELEM
 #undef BGX_LAUNDER_Z
+#undef BGX_TILE_ON
+#undef BGX_TILE_T
+#undef BGX_DZ
     // each lane of half 0 holds the fp32 sums of its own rows (a few dozen per lane);
     // the wave and the workgroup add them in fp64
     double dp = (double)s_pol, dvv = (double)s_val, de = (double)s_ent;
@@ -362,7 +443,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     __syncthreads();
     if (threadIdx.x < 3) {
         double t = 0.0;
-        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i][threadIdx.x];
+        for (int i = 0; i < kW; ++i) t += red[i][threadIdx.x];
         atomicAdd(a.sums + threadIdx.x, t);
     }
 }
@@ -407,19 +488,40 @@ __global__ __launch_bounds__(256) void k_ppo_gw2(Gw2Args a) {
         for (int i = 0; i < 16; ++i) acc[u][i] = 0.0f;
     float gb = 0.0f;
     uint8_t* img = sh[wv];
-    for (int tile = tile0; tile < tile1; ++tile) {
-        const int pos = tile * 32 + r;
-        const bool valid = pos < a.m;
-        const int row = a.perm[valid ? pos : a.m - 1];
-        const uint4* hp = (const uint4*)(a.h + (size_t)row * kH);
-        uint4 ha[8];                                                        // A operand: h[row][16s + 8hh + j]
+    // software pipeline: the row index two tiles ahead, the h row and statistics one
+    // tile ahead (the loop is otherwise bound by the latency of its dependent loads)
+    auto row_of = [&](int tile) {
+        const int pos = tile * 32 + r, p = pos < a.m ? pos : a.m - 1;
+        return a.perm ? a.perm[p] : p;
+    };
+    uint4 ha[8];                                                            // A operand: h[row][16s + 8hh + j]
+    float4 stc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    int infc = 0, row_nn = 0;
+    if (tile0 < tile1) {
+        const uint4* hp = (const uint4*)(a.h + (size_t)row_of(tile0) * kH);
         #pragma unroll
         for (int s = 0; s < 8; ++s) ha[s] = hp[2 * s + hh];
+        const int pos = tile0 * 32 + r;
+        if (pos < a.m) { stc = a.stats[pos]; infc = a.info[pos]; }          // else lim 0: nothing in play
+        if (tile0 + 1 < tile1) row_nn = row_of(tile0 + 1);
+    }
+    for (int tile = tile0; tile < tile1; ++tile) {
+        uint4 hn[8];
+        float4 stn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        int infn = 0, row_n3 = 0;
+        if (tile + 1 < tile1) {
+            const uint4* hp = (const uint4*)(a.h + (size_t)row_nn * kH);
+            #pragma unroll
+            for (int s = 0; s < 8; ++s) hn[s] = hp[2 * s + hh];
+            const int pos = (tile + 1) * 32 + r;
+            if (pos < a.m) { stn = a.stats[pos]; infn = a.info[pos]; }
+            if (tile + 2 < tile1) row_n3 = row_of(tile + 2);
+        }
         #pragma unroll
         for (int s = 0; s < 8; ++s) *(uint4*)(img + swz(r, 2 * s + hh)) = ha[s];
         if (hh == 0) {
-            sst[wv][r] = valid ? a.stats[pos] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            sinf[wv][r] = valid ? a.info[pos] : 0;                          // lim 0: nothing in play
+            sst[wv][r] = stc;
+            sinf[wv][r] = infc;
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -459,6 +561,11 @@ __global__ __launch_bounds__(256) void k_ppo_gw2(Gw2Args a) {
                 acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afr, tr_operand(img, 0, s, u, l), acc[u], 0, 0, 0);
         }
         __builtin_amdgcn_wave_barrier();                                    // tile reads done before the next stores
+        #pragma unroll
+        for (int s = 0; s < 8; ++s) ha[s] = hn[s];
+        stc = stn;
+        infc = infn;
+        row_nn = row_n3;
     }
     gb = hsum(gb);
     // C = gW2 tile: lane = hidden 32u + r, register i = action row (i&3) + 8(i>>2) + 4hh
@@ -470,14 +577,34 @@ __global__ __launch_bounds__(256) void k_ppo_gw2(Gw2Args a) {
     if (hh == 0) out[32 * kH + r] = gb;
 }
 
-// gW2[32at + i][c] += sum over the action tile's tasks of their partials (fixed order)
-__global__ __launch_bounds__(256) void k_ppo_gw2_reduce(const float* __restrict__ part, const int32_t* __restrict__ plan,
-                                                        float* __restrict__ gw2, float* __restrict__ gb2) {
+// gW2[32at + i][c] += sum over the action tile's tasks of their partials, in a fixed
+// order: k_ppo_gw2_sum1 sums the tasks of residue g mod kRed (8-way unrolled
+// independent loads), k_ppo_gw2_sum2 the kRed group sums.
+constexpr int kRed = 32;
+__global__ __launch_bounds__(256) void k_ppo_gw2_sum1(const float* __restrict__ part, const int32_t* __restrict__ plan,
+                                                      float* __restrict__ part2) {
+    const int at = blockIdx.y, g = blockIdx.z;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kPart) return;
+    const int t0 = plan[at] + g, t1 = plan[at + 1];
+    float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int t = t0;
+    for (; t + 7 * kRed < t1; t += 8 * kRed) {
+        #pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += part[(size_t)(t + k * kRed) * kPart + e];
+    }
+    for (int k = 0; t < t1; t += kRed, ++k) acc[k] += part[(size_t)t * kPart + e];
+    part2[((size_t)at * kRed + g) * kPart + e] =
+        ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+__global__ __launch_bounds__(256) void k_ppo_gw2_sum2(const float* __restrict__ part2, float* __restrict__ gw2,
+                                                      float* __restrict__ gb2) {
     const int at = blockIdx.y;
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= kPart) return;
     float s = 0.0f;
-    for (int t = plan[at]; t < plan[at + 1]; ++t) s += part[(size_t)t * kPart + e];
+    #pragma unroll 8
+    for (int g = 0; g < kRed; ++g) s += part2[((size_t)at * kRed + g) * kPart + e];
     if (e < 32 * kH) gw2[(size_t)(32 * at) * kH + e] += s;
     else gb2[32 * at + (e - 32 * kH)] += s;
 }
@@ -490,20 +617,29 @@ extern "C" int bgx_ppo_rows(const void* h, const int32_t* perm, const uint8_t* r
                             const float* old_logp, const float* returns, const float* adv, int32_t m, int32_t hidden,
                             int32_t n_actions, const void* w2h, const void* b2h, float eps_clip, float c_value,
                             float c_entropy, float grad_scale, void* dh, void* stats, int32_t* info, double* sums,
-                            void* dy, int32_t grid, void* stream) {
+                            void* dy, const int32_t* row_plan, int32_t grid, void* stream) {
     if (hidden != kH || n_actions != kA || m < 0) return BGX_EINVAL;
     if (m == 0) return BGX_OK;
-    if (!h || !perm || !records || !actions || !old_logp || !returns || !adv || !w2h || !b2h || !dh || !stats ||
-        !info || !sums)
+    if (!h || !records || !actions || !old_logp || !returns || !adv || !w2h || !b2h || !dh || !stats ||
+        !info || !sums || !row_plan)
         return BGX_EINVAL;
     if (((uintptr_t)h | (uintptr_t)w2h | (uintptr_t)stats | (uintptr_t)dy) % 16 || ((uintptr_t)dh | (uintptr_t)b2h) % 8)
         return BGX_EINVAL;
-    const int wgs = (m + 255) / 256;
-    const int g = grid > 0 ? grid : 256;
     RowsArgs a{(const _Float16*)h, perm, records, actions, old_logp, returns, adv, (const _Float16*)w2h,
                (const _Float16*)b2h, m, eps_clip, c_value, c_entropy, grad_scale, (_Float16*)dh, (float4*)stats,
                info, sums, (_Float16*)dy};
-    hipLaunchKernelGGL(k_ppo_rows, dim3(wgs < g ? wgs : g), dim3(512), 0, (hipStream_t)stream, a);
+    hipStream_t s = (hipStream_t)stream;
+    const int ntiles = (m + 31) / 32;
+    // persistent grids: at most enough workgroups for every row tile, else `grid` (<= 0:
+    // 4 per CU for the small variants, 1 per CU for the 16-tile one)
+    auto wgs = [&](int waves, int dflt) {
+        const int need = (ntiles + waves - 1) / waves, g = grid > 0 ? grid : dflt;
+        return dim3(need < g ? need : g);
+    };
+    hipLaunchKernelGGL(k_ppo_rows<1>, wgs(4, 1024), dim3(256), 0, s, a, row_plan + 0);
+    hipLaunchKernelGGL(k_ppo_rows<2>, wgs(4, 1024), dim3(256), 0, s, a, row_plan + 2);
+    hipLaunchKernelGGL(k_ppo_rows<4>, wgs(4, 1024), dim3(256), 0, s, a, row_plan + 4);
+    hipLaunchKernelGGL(k_ppo_rows<kNT>, wgs(8, 256), dim3(512), 0, s, a, row_plan + 6);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }
@@ -511,7 +647,8 @@ extern "C" int bgx_ppo_rows(const void* h, const int32_t* perm, const uint8_t* r
 extern "C" int64_t bgx_ppo_gw2_workspace(int32_t m) {
     if (m < 0) return BGX_EINVAL;
     const int64_t ntiles = (m + 31) / 32;
-    return (int64_t)kNT * ((ntiles + kTS - 1) / kTS) * kPart * (int64_t)sizeof(float);
+    // task partials, then kRed group sums per action tile
+    return ((int64_t)kNT * ((ntiles + kTS - 1) / kTS) + (int64_t)kNT * kRed) * kPart * (int64_t)sizeof(float);
 }
 
 extern "C" int bgx_ppo_gw2(const void* h, const int32_t* perm, const void* stats, const int32_t* info, int32_t m,
@@ -519,7 +656,7 @@ extern "C" int bgx_ppo_gw2(const void* h, const int32_t* perm, const void* stats
                            const int32_t* plan, float* workspace, float* gw2, float* gb2, void* stream) {
     if (hidden != kH || n_actions != kA || m < 0) return BGX_EINVAL;
     if (m == 0) return BGX_OK;
-    if (!h || !perm || !stats || !info || !w2h || !b2h || !plan || !workspace || !gw2 || !gb2) return BGX_EINVAL;
+    if (!h || !stats || !info || !w2h || !b2h || !plan || !workspace || !gw2 || !gb2) return BGX_EINVAL;
     if (((uintptr_t)h | (uintptr_t)w2h | (uintptr_t)stats) % 16) return BGX_EINVAL;
     const int ntiles = (m + 31) / 32;
     const int max_tasks = kNT * ((ntiles + kTS - 1) / kTS);
@@ -527,7 +664,9 @@ extern "C" int bgx_ppo_gw2(const void* h, const int32_t* perm, const void* stats
               plan, workspace};
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(k_ppo_gw2, dim3((max_tasks + 3) / 4), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_ppo_gw2_reduce, dim3((kPart + 255) / 256, kNT), dim3(256), 0, s, workspace, plan, gw2, gb2);
+    float* part2 = workspace + (size_t)max_tasks * kPart;
+    hipLaunchKernelGGL(k_ppo_gw2_sum1, dim3((kPart + 255) / 256, kNT, kRed), dim3(256), 0, s, workspace, plan, part2);
+    hipLaunchKernelGGL(k_ppo_gw2_sum2, dim3((kPart + 255) / 256, kNT), dim3(256), 0, s, part2, gw2, gb2);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }

@@ -40,7 +40,7 @@ def _p(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def _fused(recs, acts, old, R, adv, W2h, b2h, h, coefs, perm, plan, want_dy=True):
+def _fused(recs, acts, old, R, adv, W2h, b2h, h, coefs, perm, plan, row_plan, want_dy=True):
     from bgx import _lib
     from bgx._lib import check
     L = _lib.load()
@@ -53,7 +53,8 @@ def _fused(recs, acts, old, R, adv, W2h, b2h, h, coefs, perm, plan, want_dy=True
     dy = torch.full((m, 512), float("nan"), dtype=torch.float16, device="cuda") if want_dy else None
     eps, cv, ce, gs = coefs
     check(L.bgx_ppo_rows(_p(h), _p(perm), _p(recs), _p(acts), _p(old), _p(R), _p(adv), m, 128, 500, _p(W2h), _p(b2h),
-                         eps, cv, ce, gs, _p(dh), _p(stats), _p(info), _p(sums), _p(dy), 0, s), "bgx_ppo_rows")
+                         eps, cv, ce, gs, _p(dh), _p(stats), _p(info), _p(sums), _p(dy), _p(row_plan), 0, s),
+          "bgx_ppo_rows")
     gw2 = torch.zeros(512, 128, dtype=torch.float32, device="cuda")
     gb2 = torch.zeros(512, dtype=torch.float32, device="cuda")
     ws = torch.empty(L.bgx_ppo_gw2_workspace(m) // 4, dtype=torch.float32, device="cuda")
@@ -97,8 +98,8 @@ def test_fused_head_matches_round2_composition():
     from bgx.train import ppo_row_plan
     args = _setup()
     recs = args[0]
-    perm, plan = ppo_row_plan(recs)
-    dh, dy, gw2, gb2, sums = _fused(*args, COEFS, perm, plan)
+    perm, plan, row_plan = ppo_row_plan(recs)
+    dh, dy, gw2, gb2, sums = _fused(*args, COEFS, perm, plan, row_plan)
     rdh, rdy, rgw2, rgb2, rsums = _reference(*args, COEFS)
     # loss sums: the same per-row formulas; fp32 log-sum-exp in another order
     m = recs.shape[0]
@@ -131,15 +132,17 @@ def test_fused_head_row_order_invariant():
     args = _setup(seed=3, batch=2048, horizon=5)
     recs = args[0]
     m = recs.shape[0]
-    perm, plan = ppo_row_plan(recs)
-    a = _fused(*args, COEFS, perm, plan)
+    perm, plan, row_plan = ppo_row_plan(recs)
+    a = _fused(*args, COEFS, perm, plan, row_plan)
     ident = torch.arange(m, dtype=torch.int32, device="cuda")
     ntiles = (m + 31) // 32
     tasks = (ntiles + 31) // 32
     plan2 = torch.tensor([tasks * i for i in range(17)] + [0] * 16, dtype=torch.int32, device="cuda")
     rev = torch.flip(ident, [0]).contiguous()
+    # unsorted rows: every row tile through the 16-tile variant
+    rp2 = torch.tensor([0, 0, 0, 0, 0, 0, 0, ntiles], dtype=torch.int32, device="cuda")
     for p2 in (ident, rev):
-        b = _fused(*args, COEFS, p2, plan2)
+        b = _fused(*args, COEFS, p2, plan2, rp2)
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
         assert _rel(b[2], a[2]) < 1e-6 and _rel(b[3], a[3]) < 1e-6
         assert torch.allclose(a[4] / m, b[4] / m, rtol=1e-6, atol=1e-7)

@@ -7,8 +7,8 @@ import test_gpu_ppo_fused as T  # noqa: E402
 from bgx.train import ppo_row_plan  # noqa: E402
 args = T._setup()
 recs, h = args[0], args[-1]
-perm, plan = ppo_row_plan(recs)
-dh, dy, gw2, gb2, sums = T._fused(*args, T.COEFS, perm, plan)
+perm, plan, row_plan = ppo_row_plan(recs)
+dh, dy, gw2, gb2, sums = T._fused(*args, T.COEFS, perm, plan, row_plan)
 rdh, rdy, rgw2, rgb2, rsums = T._reference(*args, T.COEFS)
 print("sums", sums.tolist(), rsums.tolist())
 print("dy rel", T._rel(dy, rdy), "dh rel", T._rel(dh, rdh), "gw2 rel", T._rel(gw2, rgw2), "gb2 rel", T._rel(gb2, rgb2))
