@@ -698,19 +698,45 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
     #pragma unroll 1
     for (int g0 = 0; g0 < NT; g0 += G) {
         f32x16 x[2][G];
+#if BGX_EVAL_PIPE
+        // the next k-block's weight fragments are read while this k-block's MFMAs run
+        // (LLVM otherwise issues each ds_read_b128 one or two MFMAs before its use and
+        // the wave waits on lgkmcnt; sched_barrier pins the order)
+        uint4 abuf[G], nbuf[G];
+        #pragma unroll
+        for (int t = 0; t < G; ++t) abuf[t] = g0 + t < NT ? wq[(g0 + t) * 64 + l + z] : make_uint4(0, 0, 0, 0);
+#endif
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) {
+#if BGX_EVAL_PIPE
+            if (kb + 1 < kKB) {
+                #pragma unroll
+                for (int t = 0; t < G; ++t)
+                    if (g0 + t < NT) nbuf[t] = wq[((kb + 1) * NT + g0 + t) * 64 + l + z];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
             #pragma unroll
             for (int t = 0; t < G; ++t) {
                 if (g0 + t < NT) {
+#if BGX_EVAL_PIPE
+                    const f16x8 a = __builtin_bit_cast(f16x8, abuf[t]);
+#else
                     const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + g0 + t) * 64 + l + z]);
+#endif
                     const f32x16 c0 = kb == 0 ? (f32x16){} : x[0][t];
                     const f32x16 c1 = kb == 0 ? (f32x16){} : x[1][t];
                     x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, c0, 0, 0, 0);
                     x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, c1, 0, 0, 0);
                 }
             }
+#if BGX_EVAL_PIPE
+            if (kb + 1 < kKB) {
+                #pragma unroll
+                for (int t = 0; t < G; ++t) abuf[t] = nbuf[t];
+            }
+#endif
         }
         #pragma unroll
         for (int n = 0; n < 2; ++n)
@@ -728,10 +754,62 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
     for (int n = 0; n < 2; ++n) v[n] += __shfl_xor(v[n], 32) + bias;
 }
 
+// H > 64 (NT > 4 unit tiles): one 32-leaf tile at a time with ALL unit tiles'
+// accumulators live (NT x 16 VGPRs), so each k-block's features are generated once
+// (the two-tile form regenerated them in a second pass over K: twice the VALU feature
+// work, which kept the MFMA pipe ~half idle at H = 128).  The weight fragments are
+// read once per 32 leaves instead of once per 64 (one ds_read_b128 per MFMA).
+template <int NT, int G>
+__device__ __forceinline__ float eval_leaf_tile(const uint4* wq, const float* wvs, const Leaf& L, int z, float bias) {
+    const int l = lane_id(), h = l >> 5;
+    float v = 0.0f;
+    #pragma unroll 1
+    for (int g0 = 0; g0 < NT; g0 += G) {
+        f32x16 x[G];
+        #pragma unroll
+        for (int kb = 0; kb < kKB; ++kb) {
+            const f16x8 f = feat16(L, kb, h);
+            #pragma unroll
+            for (int t = 0; t < G; ++t) {
+                const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + g0 + t) * 64 + l + z]);
+                x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+            }
+        }
+        #pragma unroll
+        for (int t = 0; t < G; ++t)
+            #pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int r = j < 4 ? j : j + 4;
+                v = fmaf(fmaxf(x[t][r] + x[t][r + 4], 0.0f), wvs[((g0 + t) * 8 + j) * 64 + l + z], v);
+            }
+    }
+    return v + __shfl_xor(v, 32) + bias;
+}
+
 // workgroup shape of the evaluators: 4 waves (NT <= 4: <= 52 KiB of weights in LDS,
 // several workgroups per CU) or 8 waves (H = 128: 120 KiB, one workgroup per CU,
 // two waves per SIMD)
-template <int NT> struct EvalShape { static constexpr int kWaves = NT <= 4 ? 4 : 8; };
+#ifndef BGX_EVAL_WIDE_WAVES
+#define BGX_EVAL_WIDE_WAVES 8
+#endif
+#ifndef BGX_EVAL_PIPE
+#define BGX_EVAL_PIPE 0
+#endif
+#ifndef BGX_EVAL_G
+#define BGX_EVAL_G 4
+#endif
+#ifndef BGX_EVAL_NARROW_WAVES
+#define BGX_EVAL_NARROW_WAVES 4
+#endif
+#ifndef BGX_EVAL_SINGLE_MIN_NT
+#define BGX_EVAL_SINGLE_MIN_NT 99
+#endif
+constexpr int kEvalG = BGX_EVAL_G;           // unit tiles accumulated per pass (single-tile form)
+template <int NT> struct EvalShape {
+    static constexpr int kWaves = NT <= 4 ? BGX_EVAL_NARROW_WAVES : BGX_EVAL_WIDE_WAVES;
+    static constexpr bool kSingle = NT >= BGX_EVAL_SINGLE_MIN_NT;   // one 32-leaf tile per call
+    static constexpr int kG = NT < kEvalG ? NT : kEvalG;
+};
 
 template <int NT>
 __device__ __forceinline__ void stage_weights(uint4* wq, float* wvs, const uint4* w1q, const float* wvq) {
@@ -771,7 +849,16 @@ __global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) void k_eval(EvalArgs E)
         #pragma unroll
         for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
         float v[2];
-        eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
+        if (EvalShape<NT>::kSingle) {
+            // the second tile's weight reads depend on the first tile's value (an opaque
+            // zero offset): LLVM cannot interleave the two 128-accumulator chains
+            v[0] = eval_leaf_tile<NT, EvalShape<NT>::kG>(wq, wvs, L[0], z, E.bv);
+            int z2 = z;
+            __asm__ volatile("" : "+s"(z2) : "v"(v[0]));
+            v[1] = eval_leaf_tile<NT, EvalShape<NT>::kG>(wq, wvs, L[1], z2, E.bv);
+        } else {
+            eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
+        }
         #pragma unroll
         for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
         #pragma unroll
@@ -996,7 +1083,8 @@ static EvalRowsFn eval_rows_kernel(int NT) {
         case 7: return k_eval_rows<7>; default: return k_eval_rows<8>;
     }
 }
-static int eval_waves(int NT) { return NT <= 4 ? 4 : 8; }
+// the launch's workgroup size must be the kernels' EvalShape<NT>::kWaves (their tile stride)
+static int eval_waves(int NT) { return NT <= 4 ? BGX_EVAL_NARROW_WAVES : BGX_EVAL_WIDE_WAVES; }
 
 // resident workgroups of an evaluator over the whole device
 template <typename K>
