@@ -105,7 +105,8 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
     const int j0 = C * c32;                                 // this lane's columns j0 .. j0+15
     const bool vload = vec && j0 + C <= ld_logits;
     const bool vstore = vec && j0 + C <= ld_dlogits && (pad || j0 + C <= A);
-    float s_pol = 0.0f, s_val = 0.0f, s_ent = 0.0f, s_gv = 0.0f;   // per-half partials (<= a few hundred rows)
+    // per-half loss partials in fp64: a call may give one half thousands of rows
+    double s_pol = 0.0, s_val = 0.0, s_ent = 0.0;
     float cs[C];
     #pragma unroll
     for (int i = 0; i < C; ++i) cs[i] = 0.0f;
@@ -176,7 +177,8 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
         const float dv = v - ret;
         const float gv = gscale * c_value * 2.0f * dv;
         // past A, p = 0 and g = 0: with `pad` the stored layout [logits | value | 0]
-        // gets the value gradient in column A (lane 0, after the row's vector stores)
+        // gets the value gradient in column A, written by the lane that owns that
+        // column in the same store as its other columns (one writer per address)
         T* dl = dlogits + (int64_t)row * ld_dlogits;
         if (vstore) {
             #pragma unroll
@@ -185,7 +187,8 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
                 t4 w;
                 #pragma unroll
                 for (int i = 4 * k; i < 4 * k + 4; ++i) {
-                    const T t = (T)fmaf(z[i], fmaf(k1, q[i], k2), j0 + i == act ? gla : 0.0f);
+                    const float g = pad && j0 + i == A ? gv : fmaf(z[i], fmaf(k1, q[i], k2), j0 + i == act ? gla : 0.0f);
+                    const T t = (T)g;
                     w[i - 4 * k] = t;
                     cs[i] += (float)t;
                 }
@@ -195,30 +198,26 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
             #pragma unroll
             for (int i = 0; i < C; ++i) {
                 const int j = j0 + i;
-                if (j < A || (pad && j < ld_dlogits && j != A)) {
-                    const T t = (T)fmaf(z[i], fmaf(k1, q[i], k2), j == act ? gla : 0.0f);
+                if (j < A || (pad && j < ld_dlogits)) {
+                    const float g = j == A ? gv : fmaf(z[i], fmaf(k1, q[i], k2), j == act ? gla : 0.0f);
+                    const T t = (T)g;
                     dl[j] = t;
                     cs[i] += (float)t;
                 }
             }
         }
-        if (pad && c32 == 0) {
-            const T t = (T)gv;
-            dl[A] = t;
-            s_gv += (float)t;
-        }
         if (c32 == 0) {
             dvalues[row] = (T)gv;
-            s_pol += pol;
-            s_val += dv * dv;
-            s_ent += ent;
+            s_pol += (double)pol;
+            s_val += (double)dv * (double)dv;
+            s_ent += (double)ent;
         }
     }
     // one set of double atomics per workgroup (per-wave atomics on three addresses
     // serialised: measured 2.5 ms per 1M rows)
     __shared__ double red[8][3];
     const int half = threadIdx.x >> 5;
-    if (c32 == 0) { red[half][0] = (double)s_pol; red[half][1] = (double)s_val; red[half][2] = (double)s_ent; }
+    if (c32 == 0) { red[half][0] = s_pol; red[half][1] = s_val; red[half][2] = s_ent; }
     __syncthreads();
     if (threadIdx.x < 3) {
         double t = 0.0;
@@ -229,8 +228,6 @@ __global__ __launch_bounds__(256, 4) void k_ppo_head(const T* __restrict__ logit
         __shared__ float cred[8][512];
         #pragma unroll
         for (int i = 0; i < C; ++i) cred[half][j0 + i] = cs[i];
-        __syncthreads();
-        if (pad && c32 == 0) cred[half][A] += s_gv;      // column A: the stored value gradients
         __syncthreads();
         for (int c = threadIdx.x; c < 512; c += blockDim.x) {
             float t = 0.0f;

@@ -43,6 +43,26 @@
 
 using namespace bg;
 
+// evaluator build knobs (A/B: tools/build_variant.sh + tools/ab_eval.sh)
+#ifndef BGX_EVAL_WIDE_WAVES
+#define BGX_EVAL_WIDE_WAVES 8
+#endif
+#ifndef BGX_EVAL_PIPE
+#define BGX_EVAL_PIPE 0
+#endif
+#ifndef BGX_EVAL_SKIP
+#define BGX_EVAL_SKIP 0
+#endif
+#ifndef BGX_EVAL_G
+#define BGX_EVAL_G 4
+#endif
+#ifndef BGX_EVAL_NARROW_WAVES
+#define BGX_EVAL_NARROW_WAVES 4
+#endif
+#ifndef BGX_EVAL_SINGLE_MIN_NT
+#define BGX_EVAL_SINGLE_MIN_NT 99
+#endif
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -653,15 +673,19 @@ __device__ __forceinline__ uint4 units_pair(uint32_t byte) {
     return make_uint4(u0, u1, u2, f16_pair(x3, 0.5f, 0.5f));
 }
 
+// the two point counts (nibbles) k-block kb < 12 takes from this lane's half h:
+// points 4 k6 + 2h, +1 = byte (2 k6 + h) of the player's 96-bit nibble vector
+__device__ __forceinline__ uint32_t kb_byte(const Leaf& L, int kb, int h) {
+    const int P = kb / 6, k6 = kb % 6;
+    const uint32_t dw = k6 < 2 ? (uint32_t)L.lo[P] : (k6 < 4 ? (uint32_t)(L.lo[P] >> 32) : L.hi[P]);
+    return (dw >> (16 * (k6 & 1) + 8 * h)) & 0xFFu;
+}
+
 // B operand of k-block kb for this lane's half h (permuted K order, kperm)
 __device__ __forceinline__ f16x8 feat16(const Leaf& L, int kb, int h) {
     uint4 v;
     if (kb < 12) {
-        const int P = kb / 6, k6 = kb % 6;
-        // points 4 k6 + 2h, +1: byte (2 k6 + h) of the 96-bit nibble vector
-        const uint32_t dw = k6 < 2 ? (uint32_t)L.lo[P] : (k6 < 4 ? (uint32_t)(L.lo[P] >> 32) : L.hi[P]);
-        const uint32_t byte = (dw >> (16 * (k6 & 1) + 8 * h)) & 0xFFu;
-        v = units_pair(byte);
+        v = units_pair(kb_byte(L, kb, h));
     } else if (h == 0) {
         v = make_uint4(f16_pair(L.bar[0] | (L.off[0] << 16), 0.5f, 1.0f),
                        f16_pair(L.bar[1] | (L.off[1] << 16), 0.5f, 1.0f),
@@ -706,6 +730,12 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
         #pragma unroll
         for (int t = 0; t < G; ++t) abuf[t] = g0 + t < NT ? wq[(g0 + t) * 64 + l + z] : make_uint4(0, 0, 0, 0);
 #endif
+#if BGX_EVAL_SKIP
+        #pragma unroll
+        for (int n = 0; n < 2; ++n)
+            #pragma unroll
+            for (int t = 0; t < G; ++t) x[n][t] = (f32x16){};
+#endif
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) {
 #if BGX_EVAL_PIPE
@@ -717,6 +747,16 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
             __builtin_amdgcn_sched_barrier(0);
 #endif
             const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
+#if BGX_EVAL_SKIP
+            // exact: a k-block whose 4 points are empty in all 32 leaves of a tile has
+            // all-zero features there, and its products add exactly 0 to the
+            // accumulators (finite weights).  Leaves of a tile share their job's root
+            // afterstate, so whole 4-point groups are often empty (mean 4 of 12 per board)
+            const bool on0 = kb >= 12 || __ballot(kb_byte(L[0], kb < 12 ? kb : 0, h) != 0u) != 0ull;
+            const bool on1 = kb >= 12 || __ballot(kb_byte(L[1], kb < 12 ? kb : 0, h) != 0u) != 0ull;
+#else
+            const bool on0 = true, on1 = true;
+#endif
             #pragma unroll
             for (int t = 0; t < G; ++t) {
                 if (g0 + t < NT) {
@@ -725,10 +765,16 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
 #else
                     const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + g0 + t) * 64 + l + z]);
 #endif
+#if BGX_EVAL_SKIP
+                    if (on0) x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, x[0][t], 0, 0, 0);
+                    if (on1) x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, x[1][t], 0, 0, 0);
+#else
+                    (void)on0; (void)on1;
                     const f32x16 c0 = kb == 0 ? (f32x16){} : x[0][t];
                     const f32x16 c1 = kb == 0 ? (f32x16){} : x[1][t];
                     x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, c0, 0, 0, 0);
                     x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, c1, 0, 0, 0);
+#endif
                 }
             }
 #if BGX_EVAL_PIPE
@@ -789,21 +835,6 @@ __device__ __forceinline__ float eval_leaf_tile(const uint4* wq, const float* wv
 // workgroup shape of the evaluators: 4 waves (NT <= 4: <= 52 KiB of weights in LDS,
 // several workgroups per CU) or 8 waves (H = 128: 120 KiB, one workgroup per CU,
 // two waves per SIMD)
-#ifndef BGX_EVAL_WIDE_WAVES
-#define BGX_EVAL_WIDE_WAVES 8
-#endif
-#ifndef BGX_EVAL_PIPE
-#define BGX_EVAL_PIPE 0
-#endif
-#ifndef BGX_EVAL_G
-#define BGX_EVAL_G 4
-#endif
-#ifndef BGX_EVAL_NARROW_WAVES
-#define BGX_EVAL_NARROW_WAVES 4
-#endif
-#ifndef BGX_EVAL_SINGLE_MIN_NT
-#define BGX_EVAL_SINGLE_MIN_NT 99
-#endif
 constexpr int kEvalG = BGX_EVAL_G;           // unit tiles accumulated per pass (single-tile form)
 template <int NT> struct EvalShape {
     static constexpr int kWaves = NT <= 4 ? BGX_EVAL_NARROW_WAVES : BGX_EVAL_WIDE_WAVES;
@@ -824,7 +855,8 @@ __device__ __forceinline__ void stage_weights(uint4* wq, float* wvs, const uint4
 // wave walks its own tiles with the next tile's pool entries in flight during the
 // current tile's MFMAs.
 template <int NT>
-__global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) void k_eval(EvalArgs E) {
+__global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) __attribute__((amdgpu_waves_per_eu(NT <= 4 ? 3 : 2)))
+void k_eval(EvalArgs E) {
     constexpr int W = EvalShape<NT>::kWaves;
     __shared__ uint4 wq[kKB * NT * 64];
     __shared__ float wvs[NT * 8 * 64];
