@@ -569,6 +569,12 @@ def main():
         line["two_ply"] = two_ply_bench(eng2, args.two_ply_batches, ws, dev)
         # the same roots with the reference's H = 128 value head (agent/config.py:8)
         line["two_ply_h128"] = two_ply_bench(eng2, 1, ws, dev, hidden=128)
+        if eng2 is not engs[0]:             # its 2-ply leaf pool and workspaces (~11 GB) go back
+            del eng2
+            import gc
+            gc.collect()
+            torch.cuda.synchronize(dev)
+            torch.cuda.empty_cache()
     if args.c2_steps > 0:
         line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev, args.c2_shards,
                                                           not args.no_graphs)
