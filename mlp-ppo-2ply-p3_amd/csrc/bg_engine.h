@@ -432,8 +432,10 @@ struct bgx_engine {
     // (Args::ovf_count) and its k_order_count zeroes the other set for the next
     // step, so the step needs no separate memset launch
     hipStream_t step_side;      // BGX_STEP_OVERLAP: light launch beside the heavy one
-    hipEvent_t step_ev[2];
+    hipEvent_t step_ev[4];      // fork, light done, heavy done, dispatch order done
+    bool order_pending;         // the next step's launches wait for step_ev[3]
     int step_overlap;
+    bool order_async;           // BGX_ORDER_ASYNC
     int32_t* ovf_base;
     int ovf_parity;
     bool ovf_next_zeroed;

@@ -578,6 +578,9 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     e->split = !(sp && sp[0] == '0');
     const char* sov = getenv("BGX_STEP_OVERLAP");
     e->step_overlap = sov ? atoi(sov) : 1;
+    const char* oas = getenv("BGX_ORDER_ASYNC");     // "0": dispatch order on the caller's stream (A/B)
+    e->order_async = !(oas && oas[0] == '0');
+    e->order_pending = false;
     const char* t1g = getenv("BGX_TIER1_GRID");      // the step's first overflow tier (A/B)
     e->tier1_grid = t1g && atoi(t1g) > 0 ? atoi(t1g) : 256;
     const char* mm = getenv("BGX_MEMO_MODE");
@@ -706,6 +709,10 @@ int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void*
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
+    if (e->order_pending) {                  // a step's dispatch order still on the side stream
+        CK(hipStreamWaitEvent(s, e->step_ev[3], 0));
+        e->order_pending = false;
+    }
     if (e->ovf_next_zeroed) {             // the previous step's k_order_count zeroed the other set
         e->ovf_parity ^= 1;
         A.ovf_count = e->ovf_base + 4 * e->ovf_parity;
@@ -751,6 +758,10 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
             hipLaunchKernelGGL((k_step<2, 10>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev,
                                done_dev, info_dev, 0);
     } else {
+        if (e->order_pending) {              // the previous step's dispatch order (side stream)
+            CK(hipStreamWaitEvent(s, e->step_ev[3], 0));
+            e->order_pending = false;
+        }
         Args a = A;
         a.perm = e->perm_valid ? e->perm : nullptr;
         const int heavy = a.perm && e->split ? heavy_grid(A.B, A.xcd != 0) : A.B;
@@ -777,6 +788,17 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
             launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
             if (e->step_overlap != 2) light();
             CK(hipEventRecord(e->step_ev[1], e->step_side));
+            if (A.cls && e->order_async) {
+                // the next dispatch order on the side stream once both launches have
+                // written their classes: it runs beside this stream's overflow tiers
+                // and the caller's next policy kernel instead of before them; the
+                // next bgx_step waits for it (step_ev[3]) before its own launches
+                CK(hipEventRecord(e->step_ev[2], s));
+                CK(hipStreamWaitEvent(e->step_side, e->step_ev[2], 0));
+                launch_order(e, e->step_side);
+                CK(hipEventRecord(e->step_ev[3], e->step_side));
+                e->order_pending = true;
+            }
             CK(hipStreamWaitEvent(s, e->step_ev[1], 0));
         } else {
             launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
@@ -784,7 +806,7 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
                 hipLaunchKernelGGL((k_step<0, 8, 0, true>), dim3(A.B - heavy), dim3(64), 0, s, a, actions_dev,
                                    obs_dev, reward_dev, done_dev, info_dev, heavy);
         }
-        if (A.cls) launch_order(e, s);
+        if (A.cls && !e->order_pending) launch_order(e, s);
     }
     CKL();
     const int rc = slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
