@@ -22,6 +22,7 @@
 // ~1e-6 (tests/test_gpu_policy.py asserts 1e-5).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include "../../include/bgx.h"
 
 namespace {
@@ -157,42 +158,98 @@ __host__ __device__ inline void views(P base, int T, int OT, P& hdr, P& w1q, P& 
 }
 
 // MODE 0: sampling without the logits output (the rollout: no per-output
-// branches in the tile loop); MODE -1: greedy / logits_out as passed
+// branches in the tile loop); MODE -1: greedy / logits_out as passed.
+//
+// MODE 0 with skip_arg != 0 (round 3): masked-action tile skip.  A 32-row wave whose
+// rows have at most c legal actions needs output tiles 0 .. ceil(c/32)-1 and the
+// value tile only: every other output a < n_actions of those rows is masked,
+// z = z0 + kMaskLog with z0 <= ub = max ba + max_a |Wa[a]|_2 |h|_2 (Cauchy-Schwarz;
+// header floats 2-3).  When, for every row, ub + kMaskLog lies kSkipMargin below the
+// row's running max (its log-sum-exp terms are then below half an ulp of the sum,
+// which is >= 1) and ub + kMaskLog + kGumbelMax below the row's best Gumbel key (no
+// key of the tile can win), those tiles cannot change any output: the wave jumps to
+// the value tile.  A row with no legal move (count 0) samples from all n_actions
+// outputs, so the main waves leave such rows to 2 extra workgroups per kZWin rows
+// in the same launch (the grid's first blocks), each gathering up to 32 of the
+// window's count-0 rows; its 4 waves split the output tiles (a quarter each) and
+// wave 0 merges their partial log-sum-exp / Gumbel-max states through LDS, so the
+// extra workgroups last about as long as the skipping main waves.  A window with
+// more than kZCap count-0 rows (never at self-play's ~5 %) keeps them on its main
+// waves, unskipped.  Outputs equal the unskipped kernel's up to the log-sum-exp's
+// summation order (the noise is keyed by (row, action)); BGX_POLICY_SKIP=0 turns
+// the skip off.  MODE 0 workgroups are 4 waves: 4 x 32 rows, or one gathered set.
+constexpr int kZWin = 256, kZCap = 64;
+constexpr float kSkipMargin = 30.0f;
+
 template <int T, int MODE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_policy_act(const uint8_t* __restrict__ recs, int n,
+__global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_per_eu(2))) void k_policy_act(const uint8_t* __restrict__ recs, int n,
                                                    const float* __restrict__ packed, int n_actions, int n_otiles,
                                                    uint32_t seed_lo, uint32_t seed_hi, uint32_t step, int greedy_arg,
                                                    int32_t* act_out, float* logp_out, float* value_out,
-                                                   float* logits_arg, uint8_t* records_out) {
+                                                   float* logits_arg, uint8_t* records_out, int skip_arg) {
+    constexpr int kW = MODE == 0 ? 4 : 1;              // waves per workgroup
     const bool greedy = MODE < 0 ? greedy_arg != 0 : false;
     float* const logits_out = MODE < 0 ? logits_arg : nullptr;
-    __shared__ uint8_t srec[32 * 64];
+    const bool skip_on = MODE == 0 && skip_arg != 0;
+    __shared__ uint8_t srec_[kW][32 * 64];
+    __shared__ int zl[MODE == 0 ? kZCap : 1];
     const float *hdrf, *w1f, *b1p, *w2f, *b2p;
     views(packed, T, n_otiles, hdrf, w1f, b1p, w2f, b2p);
     const uint4* w1q = (const uint4*)w1f;
     const uint4* w2q = (const uint4*)w2f;
     const int e1 = __builtin_bit_cast(int, hdrf[0]), e2 = __builtin_bit_cast(int, hdrf[1]);
     const int l = lane_id();
-    const int row0 = blockIdx.x * 32;
-    // stage 32 records (2 KiB): lane l copies 32 bytes
+    const int j = l & 31, h = l >> 5;
+    const int wv = kW > 1 ? (int)(threadIdx.x >> 6) : 0;
+    uint8_t* const srec = srec_[wv];
+    // the extra workgroups come first in the grid: they start first
+    const int n_extra = skip_on ? 2 * ((n + kZWin - 1) / kZWin) : 0;
+    const bool extra = (int)blockIdx.x < n_extra;
+    const int row0 = (((int)blockIdx.x - n_extra) * kW + wv) * 32;
+    if (!extra && row0 >= n) return;                   // main waves: no barrier below
+    // count-0 rows of the kZWin-row window (the first kZCap of them in zl, extra waves)
+    int nzw = 0;
+    if (skip_on) {
+        const int base = (extra ? (int)blockIdx.x >> 1 : row0 / kZWin) * kZWin;
+        #pragma unroll
+        for (int k = 0; k < kZWin / 64; ++k) {
+            const int r = base + 64 * k + l;
+            const bool z = r < n && *(const uint16_t*)(recs + (size_t)r * 64 + 60) == 0;
+            const uint64_t m = __ballot(z);
+            const int pos = nzw + __popcll(m & ((1ull << l) - 1ull));
+            if (extra && wv == 0 && z && pos < kZCap) zl[pos] = r;
+            nzw += __popcll(m);
+        }
+    }
+    const int kx = extra ? ((int)blockIdx.x & 1) : 0;
+    const int nz = extra ? min(nzw - 32 * kx, 32) : 32;       // rows of this wave (extra: gathered)
+    if (extra && (nzw > kZCap || nz <= 0)) return;             // uniform in the workgroup
+    const bool self_zero = skip_on && !extra && nzw > kZCap;   // count-0 rows stay on the main wave
+    const int vt = n_actions >> 5;                     // the tile holding the value output
+    if (extra) __syncthreads();                        // zl
+    // stage 32 records (2 KiB, this wave's own copy): lane l copies 32 bytes
     {
         const int r = l >> 1, off = (l & 1) * 32;
-        const int gr = row0 + r < n ? row0 + r : n - 1;
+        const int gr = extra ? zl[32 * kx + (r < nz ? r : 0)] : (row0 + r < n ? row0 + r : n - 1);
         const uint4* src = (const uint4*)(recs + (size_t)gr * 64 + off);
         uint4* dst = (uint4*)(srec + r * 64 + off);
         const uint4 v0 = src[0], v1 = src[1];
         dst[0] = v0;
         dst[1] = v1;
-        if (records_out && row0 + r < n) {             // the rollout row's copy of the record
+        if (!extra && records_out && row0 + r < n) {   // the rollout row's copy of the record
             uint4* o = (uint4*)(records_out + (size_t)(row0 + r) * 64 + off);
             o[0] = v0;
             o[1] = v1;
         }
     }
-    __syncthreads();
-    const int j = l & 31, h = l >> 5;
+    if (kW > 1) __builtin_amdgcn_wave_barrier(); else __syncthreads();
     const uint8_t* myrec = srec + j * 64;
     const int count = (int)myrec[60] | ((int)myrec[61] << 8);
+    const bool row_ok = extra ? j < nz : row0 + j < n;
+    const int grow = extra ? zl[32 * kx + (j < nz ? j : 0)] : row0 + j;
+    // output tiles of this wave: all (main), a quarter (extra)
+    const int per = extra ? (n_otiles + kW - 1) / kW : n_otiles;
+    const int o_beg = extra ? min(wv * per, n_otiles) : 0, o_end = extra ? min(o_beg + per, n_otiles) : n_otiles;
 
     // ---- GEMM1: X1s[t] = W1s[32t.., :] . F^T + b1 * 2^e1  (= 2^e1 X1)
     f32x16 x1[T];
@@ -211,13 +268,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
     }
     // ReLU, then a per-wave scale 2^ex for the split of the hidden layer
-    float mx = 0.0f;
+    float mx = 0.0f, hn2 = 0.0f;
     #pragma unroll
     for (int t = 0; t < T; ++t)
         #pragma unroll
-        for (int r = 0; r < 16; ++r) { x1[t][r] = fmaxf(x1[t][r], 0.0f); mx = fmaxf(mx, x1[t][r]); }
+        for (int r = 0; r < 16; ++r) {
+            x1[t][r] = fmaxf(x1[t][r], 0.0f);
+            mx = fmaxf(mx, x1[t][r]);
+            if (skip_on) hn2 = fmaf(x1[t][r], x1[t][r], hn2);
+        }
     #pragma unroll
     for (int d = 1; d < 64; d <<= 1) mx = fmaxf(mx, __shfl_xor(mx, d));
+    // the skip's first skippable tile o_s (none: n_otiles) and the rows' logit bound
+    int o_s = n_otiles;
+    float ub = INFINITY;
+    if (skip_on && !extra) {
+        int cm = count;
+        #pragma unroll
+        for (int d = 1; d < 32; d <<= 1) cm = max(cm, __shfl_xor(cm, d));
+        o_s = max((cm + 31) >> 5, 1);
+        hn2 += __shfl_xor(hn2, 32);                    // the row's two lane halves
+        const float u0 = hdrf[2] + hdrf[3] * ldexpf(sqrtf(hn2), -e1);
+        ub = u0 + 1e-3f * fabsf(u0) + 1e-3f;           // rounding slack (the margin is 30)
+    }
     const int ex = scale_exp(mx);
     f16x8 xh[T][2], xl[T][2];
     #pragma unroll
@@ -238,13 +311,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     // (branch-free: outputs that are not actions of this lane enter as -inf)
     float m = -INFINITY, s = 0.0f, best = -INFINITY, bestz = 0.0f, value = 0.0f;
     int besta = 0;
-    const int grow = row0 + j;
     const uint32_t rowkey = mix32(mix32(seed_lo ^ mix32(seed_hi + 0x9E3779B9u)) ^ step) ^ (uint32_t)grow * 0x85EBCA6Bu;
     constexpr int NF = T * 2 * 2;                      // weight fragments per output tile
     uint4 w[NF];
     #pragma unroll
-    for (int f = 0; f < NF; ++f) w[f] = w2q[(size_t)f * 64 + l];
-    for (int o = 0; o < n_otiles; ++o) {
+    for (int f = 0; f < NF; ++f) w[f] = o_beg < o_end ? w2q[((size_t)o_beg * NF + f) * 64 + l] : make_uint4(0, 0, 0, 0);
+    for (int o = o_beg; o < o_end;) {
         f32x16 y;
         #pragma unroll
         for (int r = 0; r < 16; ++r) y[r] = b2p[(o * 16 + r) * 64 + l] * up;
@@ -259,11 +331,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 y = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh[t][mm], y, 0, 0, 0);
             }
         // the next tile's fragments go into the same registers once this tile's
-        // MFMAs have issued; the loads overlap the sampling math below
+        // MFMAs have issued; the loads overlap the sampling math below.  At the
+        // skippable range the value tile's are fetched (the skip usually holds).
+        const bool at_s = o + 1 == o_s && o_s < vt;
+        const int nx = at_s ? vt : o + 1;
         __asm__ volatile("" ::: "memory");
-        if (o + 1 < n_otiles) {
+        if (nx < o_end) {
             #pragma unroll
-            for (int f = 0; f < NF; ++f) w[f] = w2q[((size_t)(o + 1) * NF + f) * 64 + l];
+            for (int f = 0; f < NF; ++f) w[f] = w2q[((size_t)nx * NF + f) * 64 + l];
         }
         // lane l holds outputs a = 32o + hid(r, h), r = 0..15, of row j
         float z[16];
@@ -272,7 +347,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         for (int r = 0; r < 16; ++r) {
             const int a = 32 * o + hid(r, h);
             const float z0 = y[r] * down;
-            if (logits_out && grow < n && a <= n_actions) logits_out[(size_t)grow * (32 * n_otiles) + a] = z0;
+            if (logits_out && row_ok && a <= n_actions) logits_out[(size_t)grow * (32 * n_otiles) + a] = z0;
             value = a == n_actions ? z0 : value;
             z[r] = a < n_actions ? (a < count ? z0 : z0 + kMaskLog) : -INFINITY;
             tm = fmaxf(tm, z[r]);
@@ -301,6 +376,42 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 bestz = up_ ? z[r] : bestz;
             }
         }
+        int next = o + 1;
+        if (at_s) {
+            const float m_row = fmaxf(m, __shfl_xor(m, 32)), b_row = fmaxf(best, __shfl_xor(best, 32));
+            const bool ok = (count == 0 && !self_zero) || (ub + kMaskLog < m_row - kSkipMargin && ub + kMaskLog + kGumbelMax < b_row);
+            if (__ballot(!ok) == 0ull) {
+                next = vt;
+            } else {                                   // no skip: tile o + 1 after all
+                #pragma unroll
+                for (int f = 0; f < NF; ++f) w[f] = w2q[((size_t)(o + 1) * NF + f) * 64 + l];
+            }
+        }
+        o = next;
+    }
+    if (kW > 1 && extra) {
+        // waves 1..3 hand their per-lane states to wave 0 (same lane = same row half)
+        __shared__ float pm[kW > 1 ? kW - 1 : 1][5][64];
+        __shared__ int pa[kW > 1 ? kW - 1 : 1][64];
+        if (wv > 0) {
+            pm[wv - 1][0][l] = m; pm[wv - 1][1][l] = s; pm[wv - 1][2][l] = best; pm[wv - 1][3][l] = bestz;
+            pm[wv - 1][4][l] = value; pa[wv - 1][l] = besta;
+        }
+        __syncthreads();
+        if (wv > 0) return;
+        #pragma unroll
+        for (int q = 0; q < kW - 1; ++q) {
+            const float mq = pm[q][0][l], sq = pm[q][1][l], bq = pm[q][2][l], zq = pm[q][3][l];
+            const int aq = pa[q][l];
+            const float mn = fmaxf(m, mq);
+            if (mn != -INFINITY) s = s * fast_exp(m - mn) + sq * fast_exp(mq - mn);
+            m = mn;
+            const bool tk = bq > best || (bq == best && aq < besta);
+            best = tk ? bq : best;
+            besta = tk ? aq : besta;
+            bestz = tk ? zq : bestz;
+            value += pm[q][4][l];
+        }
     }
     // combine the two lane halves of each row (lanes j and j+32)
     const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(s, 32);
@@ -313,7 +424,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     const int a_fin = take2 ? besta2 : besta;
     const float z_fin = take2 ? bestz2 : bestz;
     const float v_fin = h == 0 ? value + value2 : 0.0f;   // the value row sits in exactly one half
-    if (h == 0 && grow < n) {
+    // count-0 rows of the main waves belong to the extra waves
+    if (h == 0 && row_ok && (extra || !skip_on || self_zero || count != 0)) {
         act_out[grow] = a_fin;
         // Categorical.log_prob = log(clamp(p, eps, 1 - eps)) (torch clamp_probs), in the log domain
         if (logp_out) logp_out[grow] = fminf(fmaxf(z_fin - (mm + logf(ss)), -15.942384719848633f),
@@ -322,24 +434,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     }
 }
 
-// max |w| of W1 and of W2 = [Wa; wv] -> header exponents (one workgroup)
-__global__ __launch_bounds__(1024) void k_policy_scale(const float* W1, const float* Wa, const float* wv, int H, int A,
-                                                       float* hdr) {
-    __shared__ float r1[16], r2[16];
+// max |w| of W1 and of W2 = [Wa; wv] -> header exponents; max ba and max_a |Wa[a]|_2
+// -> the tile skip's logit bound (one workgroup)
+__global__ __launch_bounds__(1024) void k_policy_scale(const float* W1, const float* Wa, const float* ba,
+                                                       const float* wv, int H, int A, float* hdr) {
+    __shared__ float r1[16], r2[16], r3[16], r4[16];
     const int t = threadIdx.x;
-    float m1 = 0.0f, m2 = 0.0f;
+    float m1 = 0.0f, m2 = 0.0f, bmax = -INFINITY, nmax = 0.0f;
     for (int i = t; i < H * kIn; i += 1024) m1 = fmaxf(m1, fabsf(W1[i]));
     for (int i = t; i < A * H; i += 1024) m2 = fmaxf(m2, fabsf(Wa[i]));
     for (int i = t; i < H; i += 1024) m2 = fmaxf(m2, fabsf(wv[i]));
+    for (int a = t; a < A; a += 1024) {
+        double q = 0.0;
+        for (int k = 0; k < H; ++k) q += (double)Wa[(size_t)a * H + k] * (double)Wa[(size_t)a * H + k];
+        nmax = fmaxf(nmax, (float)sqrt(q));
+        bmax = fmaxf(bmax, ba[a]);
+    }
     #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) { m1 = fmaxf(m1, __shfl_xor(m1, d)); m2 = fmaxf(m2, __shfl_xor(m2, d)); }
-    if ((t & 63) == 0) { r1[t >> 6] = m1; r2[t >> 6] = m2; }
+    for (int d = 1; d < 64; d <<= 1) {
+        m1 = fmaxf(m1, __shfl_xor(m1, d)); m2 = fmaxf(m2, __shfl_xor(m2, d));
+        bmax = fmaxf(bmax, __shfl_xor(bmax, d)); nmax = fmaxf(nmax, __shfl_xor(nmax, d));
+    }
+    if ((t & 63) == 0) { r1[t >> 6] = m1; r2[t >> 6] = m2; r3[t >> 6] = bmax; r4[t >> 6] = nmax; }
     __syncthreads();
     if (t == 0) {
-        for (int w = 1; w < 16; ++w) { m1 = fmaxf(m1, r1[w]); m2 = fmaxf(m2, r2[w]); }
+        for (int w = 1; w < 16; ++w) {
+            m1 = fmaxf(m1, r1[w]); m2 = fmaxf(m2, r2[w]); bmax = fmaxf(bmax, r3[w]); nmax = fmaxf(nmax, r4[w]);
+        }
         hdr[0] = __builtin_bit_cast(float, scale_exp(m1));
         hdr[1] = __builtin_bit_cast(float, scale_exp(m2));
-        for (int i = 2; i < kHdr; ++i) hdr[i] = 0.0f;
+        hdr[2] = bmax;                                 // -inf / nan: no skip (ub is not finite)
+        hdr[3] = nmax * (1.0f + 1.0f / 1024.0f);
+        for (int i = 4; i < kHdr; ++i) hdr[i] = 0.0f;
     }
 }
 
@@ -514,7 +640,7 @@ int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const flo
     if (total < 0 || !W1 || !b1 || !Wa || !ba || !wv || !bv || !packed) return BGX_EINVAL;
     const int T = (hidden + 31) / 32, OT = (n_actions + 1 + 31) / 32;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_policy_scale, dim3(1), dim3(1024), 0, s, W1, Wa, wv, hidden, n_actions, packed);
+    hipLaunchKernelGGL(k_policy_scale, dim3(1), dim3(1024), 0, s, W1, Wa, ba, wv, hidden, n_actions, packed);
     const int work = kKB1 * T * 64 * 8 + T * 16 * 64 + OT * T * 2 * 64 * 8 + OT * 16 * 64;
     hipLaunchKernelGGL(k_policy_pack, dim3((work + 255) / 256), dim3(256), 0, s, W1, b1, Wa, ba, wv, bv, hidden,
                        n_actions, T, OT, packed);
@@ -528,18 +654,25 @@ int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packe
         return BGX_EINVAL;
     if (n == 0) return BGX_OK;
     const int T = (hidden + 31) / 32, OT = (n_actions + 1 + 31) / 32;
-    const dim3 grid((n + 31) / 32), blk(64);
+    const int n_main = (n + 31) / 32;
+    const dim3 grid(n_main), blk(64);
+    const int n_wg = (n + 127) / 128;                  // MODE 0: 4-wave workgroups
     hipStream_t s = (hipStream_t)stream;
     const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
     const bool plain = !greedy && !logits_out;
+    // the masked-action tile skip (k_policy_act, MODE 0): 2 extra waves per kZWin rows for count-0 rows
+    const char* sv = getenv("BGX_POLICY_SKIP");     // read per call: tests compare both paths in one process
+    const bool skip = !(sv && sv[0] == '0');
+    const dim3 grid0(skip ? n_wg + 2 * ((n + kZWin - 1) / kZWin) : n_wg);
 #define BGX_ACT(TT)                                                                                           \
     do {                                                                                                      \
         if (plain)                                                                                            \
-            hipLaunchKernelGGL((k_policy_act<TT, 0>), grid, blk, 0, s, records_dev, n, packed, n_actions, OT, lo, \
-                               hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out);      \
+            hipLaunchKernelGGL((k_policy_act<TT, 0>), grid0, dim3(256), 0, s, records_dev, n, packed, n_actions, OT, \
+                               lo, hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out,   \
+                               skip ? 1 : 0);                                                                 \
         else                                                                                                  \
             hipLaunchKernelGGL((k_policy_act<TT, -1>), grid, blk, 0, s, records_dev, n, packed, n_actions, OT,   \
-                               lo, hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out);  \
+                               lo, hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out, 0); \
     } while (0)
     switch (T) {
         case 1: BGX_ACT(1); break;

@@ -174,3 +174,56 @@ def test_rollout_path_in_place(bgx):
         assert torch.equal(r1, r2) and torch.equal(d1, d2)
     assert torch.equal(e1.records(), e2.records())
     assert e1.error() == 0 and e2.error() == 0
+
+
+def _act_both(net, rec, seed, step, monkeypatch):
+    monkeypatch.setenv("BGX_POLICY_SKIP", "1")
+    on = [t.clone() for t in net.act(rec, seed=seed, step=step)]
+    monkeypatch.setenv("BGX_POLICY_SKIP", "0")
+    off = [t.clone() for t in net.act(rec, seed=seed, step=step)]
+    monkeypatch.delenv("BGX_POLICY_SKIP")
+    return on, off
+
+
+def _assert_same(on, off, rec):
+    assert torch.equal(on[0], off[0])                  # the sampled actions
+    assert torch.equal(on[2], off[2])                  # values
+    d = (on[1] - off[1]).abs()
+    zero = (rec[:, 60].int() | rec[:, 61].int()) == 0
+    assert d[~zero].max().item() <= 1e-6               # log-probs: summation order only
+    # count-0 rows: every logit carries the -103.28 mask, |z| ~ 110, one fp32 ulp 7.6e-6
+    # (as test_policy_sampling_no_legal_moves); their 4 waves' partial sums merge in LDS
+    if zero.any():
+        assert d[zero].max().item() < 4 * TOL
+
+
+def test_policy_tile_skip_matches_full_pass(bgx, monkeypatch):
+    """The masked-action tile skip and the count-0 extra waves (bg_mlp.hip,
+    k_policy_act MODE 0) give the outputs of the full 16-tile pass: self-play
+    positions (count-0 rows, doubles with hundreds of moves), a window with more
+    count-0 rows than the extra waves take, a ragged batch, and weights whose
+    logit bound is too loose for any skip."""
+    from bgx.policy import PolicyNet
+    torch.manual_seed(0)
+    net = PolicyNet(hidden_size=128).cuda()
+    eng = bgx.Engine(batch=8192, dice="philox", seed=11)
+    eng.reset()
+    zero_rows = 0
+    for i in range(24):
+        rec = eng.records()
+        zero_rows += int((rec[:, 60].int() | rec[:, 61].int()).eq(0).sum())
+        on, off = _act_both(net, rec, 7, i, monkeypatch)
+        _assert_same(on, off, rec)
+        eng.step(on[0])
+    assert zero_rows > 0
+    rec = eng.records().clone()
+    rec[300:420, 60:62] = 0                              # 120 count-0 rows in one 256-row window
+    rec[1000:1010, 60] = 244                             # 500 legal actions
+    rec[1000:1010, 61] = 1
+    _assert_same(*_act_both(net, rec, 9, 0, monkeypatch), rec)
+    _assert_same(*_act_both(net, rec[:5000 - 17], 9, 1, monkeypatch), rec[:5000 - 17])
+    big = PolicyNet(hidden_size=128).cuda()
+    with torch.no_grad():
+        big.load_state_dict(net.state_dict())
+        big.action_head.weight.mul_(40.0)
+    _assert_same(*_act_both(big, rec, 9, 2, monkeypatch), rec)

@@ -1,26 +1,37 @@
-"""Time bgx_policy_act alone on C3-shaped records (B = 65,536 lanes after a
-burn-in of self-play): sampling vs greedy, with and without the logits output."""
-import sys, os, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "mlp-ppo-2ply-p3_amd"))
-import torch, bgx
-from bgx.policy import PolicyNet
+"""Standalone time of the rollout policy kernel (bgx_policy_act, MODE 0) on
+self-play records: B lanes after some random-policy steps, skip on / off."""
+import os
+import sys
+import time
 
-B = int(os.environ.get("B", 65536))
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "mlp-ppo-2ply-p3_amd"))
+import bgx  # noqa: E402
+from bgx.policy import PolicyNet  # noqa: E402
+
+B = int(os.environ.get("B", 32768))
 torch.manual_seed(0)
 net = PolicyNet(hidden_size=128).cuda()
-eng = bgx.Engine(batch=B, dice="philox", seed=5, auto_reset=True)
-eng.reset(want_obs=False)
-for i in range(60):
-    a, _, _ = net.act(eng.records(), seed=1, step=i)
-    eng.step(a, want_obs=False)
+net.pack()
+eng = bgx.Engine(batch=B, dice="philox", seed=3, auto_reset=True)
+eng.reset()
+for i in range(40):
+    a, _, _ = net.act(eng, seed=1, step=i)
+    eng.step(a)
 rec = eng.records().clone()
-for name, kw in (("sample", {}), ("greedy", {"greedy": True})):
+cnt = (rec[:, 60].int() | (rec[:, 61].int() << 8))
+print(f"B={B} count0 {float((cnt == 0).float().mean()):.3f} >32 {float((cnt > 32).float().mean()):.3f} "
+      f">128 {float((cnt > 128).float().mean()):.3f}")
+for sk in ("1", "0", "1", "0"):
+    os.environ["BGX_POLICY_SKIP"] = sk
     for _ in range(5):
-        net.act(rec, seed=1, step=0, **kw)
+        net.act(rec, seed=2, step=0)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for i in range(50):
-        net.act(rec, seed=1, step=i, **kw)
-    e1.record(); torch.cuda.synchronize()
-    print(name, "%.1f us" % (e0.elapsed_time(e1) / 50 * 1000))
+    for k in range(50):
+        net.act(rec, seed=2, step=k)
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"skip={sk}: {e0.elapsed_time(e1) / 50 * 1e3:.1f} us per launch")
