@@ -66,7 +66,10 @@ def parse():
     ap.add_argument("--mirror-steps", type=int, default=64,
                     help="steps of the host_mirror sub-object (C3 + pinned-host copy of every row; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-graphs", action="store_true", help="C2 with eager launches instead of a HIP graph")
+    ap.add_argument("--no-graphs", action="store_true", help="C2 and C3 with eager launches instead of HIP graphs")
+    ap.add_argument("--graph-steps", type=int, default=2,
+                    help="C3: rollout steps per HIP graph (even: the engine's host state is a 2-step fixed point; "
+                         "the timed steps replay K // G graphs, the rest run eagerly)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
 
@@ -458,16 +461,74 @@ def main():
             nm_sum += sum(float(e.n_moves(out=counts[k]).float().mean().item()) for k, e in enumerate(engs)) / S
             nm_n += 1
     mean_moves = nm_sum / max(nm_n, 1)
+    # C3 as HIP graphs: one rollout step is ~20 launches and event waits over the two
+    # shards' streams and the engines' side streams, ~150 us of host time per step in
+    # eager mode (tools/c3_host_probe.py) -- close to the GPU's own step time.  Each
+    # shard's G steps are captured as a graph of their own (one graph per group of ring
+    # slots) and the shards' graphs replay on their own streams, side by side (one
+    # capture holding both shards' streams crashes the runtime at the end of capture).
+    # The policy's noise step is read from a per-shard device counter that each replay
+    # advances, so a replay is G fresh rollout steps.  Each engine is joined before the
+    # capture and at its end, so a graph holds no unjoined side-stream work and the
+    # engine's host state (overflow-counter parity, pending dispatch order) is the same
+    # before and after it (G even).  tests/test_gpu_graph.py: replays == eager steps.
+    G = args.graph_steps
+    graphs = []                                         # graphs[g][k]: slots [gG, gG + G) of shard k
+    if not args.no_graphs and args.workload == "c3" and G >= 2 and G % 2 == 0 and ring % G == 0:
+        try:
+            ctrs = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(S)]
+            caps = [torch.cuda.Stream(dev) for _ in range(S)]
+            for k in range(S):
+                with torch.cuda.stream(streams[k]):
+                    engs[k].join()
+            torch.cuda.synchronize(dev)
+            for g0 in range(0, ring, G):
+                row = []
+                for k in range(S):
+                    e, b, gr = engs[k], bufs[k], torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr, stream=caps[k]):
+                        for i in range(g0, g0 + G):
+                            net.act(e, seed=4242 + rank * 16 + k, step=i, step_ctr=ctrs[k],
+                                    out=(b["act"][i], b["logp"][i], b["value"][i]), records_out=b["records"][i])
+                            e.step(b["act"][i], want_obs=False, want_info=False, out=(b["reward"][i], b["done"][i]))
+                        e.join()
+                        PolicyNet.advance_counter(ctrs[k], ring)
+                    row.append(gr)
+                graphs.append(row)
+            torch.cuda.synchronize(dev)
+            for row in graphs:                          # untimed: first replays upload the graphs
+                for k in range(S):
+                    with torch.cuda.stream(streams[k]):
+                        row[k].replay()
+            torch.cuda.synchronize(dev)
+        except Exception as ex:
+            print(f"[bench] C3 graph capture failed ({ex}); eager", file=sys.stderr)
+            graphs = []
     torch.cuda.synchronize(dev)
     barrier(ws)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    if graphs:
+        for r in range(args.steps // G):
+            row = graphs[r % len(graphs)]
+            for k in range(S):
+                with torch.cuda.stream(streams[k]):
+                    row[k].replay()
+        for _ in range(args.steps % G):
+            step(False)
+    else:
+        for _ in range(args.steps):
+            step(True)
     torch.cuda.synchronize(dev)
     barrier(ws)
     torch.cuda.synchronize(dev)
     el_rank = time.perf_counter() - t0
+    if graphs:
+        # the roofline's kernel time: HIP events around bgx_step in eager steps right
+        # after the timed replays (events cannot be timed inside a graph)
+        for _ in range(16):
+            step(True)
+        torch.cuda.synchronize(dev)
     el = max_over_ranks(el_rank, ws)
     per_rank = gather_ranks([float(B * args.steps), el_rank], ws)
     total_steps = sum(r[0] for r in per_rank)
@@ -515,7 +576,9 @@ def main():
                    f"C1-on-GPU: B={B} games/GPU random legal policy env.step",
                    "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
                    "parallelism": f"dp{ws} (independent game shards)", "shards_per_gpu": S,
-                   "streams_per_gpu": S},
+                   "streams_per_gpu": S,
+                   "hip_graph": ({"steps_per_graph": G, "replays": args.steps // G, "eager_steps": args.steps % G}
+                                 if graphs else None)},
         "roofline": {"kernel": "env step = k_step<0,9,0,false,1> (predicted-doubles prefix) then "
                                "k_step<0,8,0,true,1> (the rest) + k_order_count/scatter + k_movegen_over tiers, "
                                "one wave per game, "

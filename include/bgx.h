@@ -53,6 +53,11 @@ enum bgx_dice_mode {
  * resets and returns done=1, backgammon_env.py:119-121). */
 int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t seed, int32_t dice_mode,
                       int32_t auto_reset, int32_t match_length, bgx_engine** out);
+/* Order `stream` after every piece of a step still running on the engine's own
+ * side streams (the next step's dispatch order): a HIP graph capture of steps
+ * calls it before capturing and as its last captured call, so the graph holds no
+ * work it does not join. */
+int bgx_engine_join(bgx_engine* e, void* stream);
 int bgx_engine_destroy(bgx_engine* e);
 
 /* BackgammonEnv.seed (backgammon_env.py:357-363): per-lane MT19937 seeds
@@ -174,6 +179,17 @@ int bgx_policy_act(const uint8_t* records_dev, int32_t n, const float* packed_de
 int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packed_dev, int32_t hidden,
                        int32_t n_actions, uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out,
                        float* logp_out, float* value_out, float* logits_out, uint8_t* records_out, void* stream);
+
+/* bgx_policy_act_rec whose noise step is step + *step_ctr, read on the device when
+ * the kernel runs (step_ctr may be NULL: then exactly bgx_policy_act_rec).  A HIP
+ * graph that captures rollout steps replays with fresh draws when the graph also
+ * advances the counter (bgx_counter_add). */
+int bgx_policy_act_ctr(const uint8_t* records_dev, int32_t n, const float* packed_dev, int32_t hidden,
+                       int32_t n_actions, uint64_t seed, uint32_t step, const uint32_t* step_ctr, int32_t greedy,
+                       int32_t* act_out, float* logp_out, float* value_out, float* logits_out, uint8_t* records_out,
+                       void* stream);
+/* *ctr_dev += v on the stream (one thread). */
+int bgx_counter_add(uint32_t* ctr_dev, uint32_t v, void* stream);
 
 /* ---- value head search: V(x) = value_head(relu(fc1 x)), H <= 128 ----
  * bgx_value_pack packs fc1.weight [H][198], fc1.bias [H], value_head.weight [H],

@@ -44,6 +44,10 @@ SIGNATURES = {
                                       _P, _P]),
     "bgx_policy_act_rec": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, ctypes.c_uint64, ctypes.c_uint32, _I32, _P, _P,
                                           _P, _P, _P, _P]),
+    "bgx_policy_act_ctr": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, ctypes.c_uint64, ctypes.c_uint32, _P, _I32, _P,
+                                          _P, _P, _P, _P, _P]),
+    "bgx_counter_add": (ctypes.c_int, [_P, ctypes.c_uint32, _P]),
+    "bgx_engine_join": (ctypes.c_int, [_P, _P]),
     "bgx_value_packed_size": (ctypes.c_int, [_I32]),
     "bgx_value_pack": (ctypes.c_int, [_P, _P, _P, _P, _I32, _P, _P]),
     "bgx_one_ply": (ctypes.c_int, [_P, _P, _I32, ctypes.c_float, _P, _P, _P, _P]),

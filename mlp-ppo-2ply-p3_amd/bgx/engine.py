@@ -135,6 +135,12 @@ class Engine:
               "bgx_step")
         return self.obs, reward, done, self.info
 
+    def join(self):
+        """Order the current stream after the engine's side-stream work (the next
+        step's dispatch order, launched asynchronously by step): call it before a
+        HIP graph capture of steps and as the capture's last call (bgx_engine_join)."""
+        check(self._lib.bgx_engine_join(self._h, self._stream()), "bgx_engine_join")
+
     # --------------------------------------------------------------- state --
     def lanes(self, lane0: int = 0, n: int | None = None):
         """(records uint8[n,64], moves int64[n,max_moves], n_total int32[n]) copies."""

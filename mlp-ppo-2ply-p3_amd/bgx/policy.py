@@ -66,14 +66,17 @@ class PolicyNet(nn.Module):
     @torch.no_grad()
     def act(self, records: torch.Tensor, seed: int = 0, step: int = 0, greedy: bool = False,
             packed: torch.Tensor | None = None, want_logits: bool = False, out=None,
-            records_out: torch.Tensor | None = None):
+            records_out: torch.Tensor | None = None, step_ctr: torch.Tensor | None = None):
         """select_action (ppo_agent.py:138-191) for every lane in ONE fused HIP
         kernel (encode -> MLP on MFMA -> masked softmax -> sample).  Returns
         (action int32[B], log_prob f32[B], value f32[B][, logits]); `out` =
         (action, log_prob, value) tensors to write instead (e.g. rows of a
         device-resident rollout buffer).  `records` may be a bgx.Engine: its
         lane records are read in place; `records_out` (uint8[B, 64]) then
-        receives the kernel's copy of them (the rollout's stored state)."""
+        receives the kernel's copy of them (the rollout's stored state).
+        `step_ctr` (int32[1] on the device): the noise's step is step + step_ctr[0]
+        read when the kernel runs, so a captured HIP graph replays with fresh draws
+        (advance it with `advance_counter`)."""
         L = _lib.load()
         packed = packed if packed is not None else getattr(self, "_packed", None)
         if packed is None:
@@ -106,13 +109,22 @@ class PolicyNet(nn.Module):
             val = torch.empty(n, dtype=torch.float32, device=dev)
         logits = torch.empty(n, 32 * ((A + 32) // 32), dtype=torch.float32, device=dev) if want_logits else None
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-        check(L.bgx_policy_act_rec(ctypes.c_void_p(rptr), n, _ptr(packed), H, A, int(seed) & (2**64 - 1),
-                                   int(step) & 0xFFFFFFFF, int(bool(greedy)), _ptr(act), _ptr(logp), _ptr(val),
-                                   _ptr(logits), _ptr(records_out), s),
-              "bgx_policy_act_rec")
+        if step_ctr is not None and (step_ctr.dtype != torch.int32 or step_ctr.device != dev or step_ctr.numel() != 1):
+            raise ValueError("act: step_ctr must be an int32[1] tensor on the records' device")
+        check(L.bgx_policy_act_ctr(ctypes.c_void_p(rptr), n, _ptr(packed), H, A, int(seed) & (2**64 - 1),
+                                   int(step) & 0xFFFFFFFF, _ptr(step_ctr), int(bool(greedy)), _ptr(act), _ptr(logp),
+                                   _ptr(val), _ptr(logits), _ptr(records_out), s),
+              "bgx_policy_act_ctr")
         if want_logits:
             return act, logp, val, logits
         return act, logp, val
+
+    @staticmethod
+    def advance_counter(step_ctr: torch.Tensor, v: int):
+        """step_ctr[0] += v on the current stream (bgx_counter_add; graph-capturable)."""
+        L = _lib.load()
+        s = ctypes.c_void_p(torch.cuda.current_stream(step_ctr.device).cuda_stream)
+        check(L.bgx_counter_add(_ptr(step_ctr), int(v) & 0xFFFFFFFF, s), "bgx_counter_add")
 
     @torch.no_grad()
     def act_torch(self, records: torch.Tensor, generator=None):

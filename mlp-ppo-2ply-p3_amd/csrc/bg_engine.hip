@@ -629,6 +629,16 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     return BGX_OK;
 }
 
+int bgx_engine_join(bgx_engine* e, void* stream) {
+    if (!e) return BGX_EINVAL;
+    CK(hipSetDevice(e->device));
+    if (e->order_pending) {                  // the next step's dispatch order, on the side stream
+        CK(hipStreamWaitEvent((hipStream_t)stream, e->step_ev[3], 0));
+        e->order_pending = false;
+    }
+    return BGX_OK;
+}
+
 int bgx_engine_destroy(bgx_engine* e) {
     if (!e) return BGX_EINVAL;
     (void)hipSetDevice(e->device);

@@ -25,6 +25,10 @@
 #include <stdlib.h>
 #include "../../include/bgx.h"
 
+#ifndef BGX_POLICY_W1_AHEAD
+#define BGX_POLICY_W1_AHEAD 2      // k-blocks of W1 fragments in flight in the policy kernel's GEMM1
+#endif
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -184,9 +188,12 @@ constexpr float kSkipMargin = 30.0f;
 template <int T, int MODE>
 __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_per_eu(2))) void k_policy_act(const uint8_t* __restrict__ recs, int n,
                                                    const float* __restrict__ packed, int n_actions, int n_otiles,
-                                                   uint32_t seed_lo, uint32_t seed_hi, uint32_t step, int greedy_arg,
+                                                   uint32_t seed_lo, uint32_t seed_hi, uint32_t step_arg,
+                                                   const uint32_t* __restrict__ step_ctr, int greedy_arg,
                                                    int32_t* act_out, float* logp_out, float* value_out,
                                                    float* logits_arg, uint8_t* records_out, int skip_arg) {
+    // the noise's step: the argument, plus a device counter when given (a replayed graph)
+    const uint32_t step = step_arg + (step_ctr ? *step_ctr : 0u);
     constexpr int kW = MODE == 0 ? 4 : 1;              // waves per workgroup
     const bool greedy = MODE < 0 ? greedy_arg != 0 : false;
     float* const logits_out = MODE < 0 ? logits_arg : nullptr;
@@ -211,10 +218,14 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
     int nzw = 0;
     if (skip_on) {
         const int base = (extra ? (int)blockIdx.x >> 1 : row0 / kZWin) * kZWin;
+        uint16_t cw[kZWin / 64];                       // all loads in flight before the first ballot
+        #pragma unroll
+        for (int k = 0; k < kZWin / 64; ++k)
+            cw[k] = *(const uint16_t*)(recs + (size_t)min(base + 64 * k + l, n - 1) * 64 + 60);
         #pragma unroll
         for (int k = 0; k < kZWin / 64; ++k) {
             const int r = base + 64 * k + l;
-            const bool z = r < n && *(const uint16_t*)(recs + (size_t)r * 64 + 60) == 0;
+            const bool z = r < n && cw[k] == 0;
             const uint64_t m = __ballot(z);
             const int pos = nzw + __popcll(m & ((1ull << l) - 1ull));
             if (extra && wv == 0 && z && pos < kZCap) zl[pos] = r;
@@ -257,12 +268,26 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
     for (int t = 0; t < T; ++t)
         #pragma unroll
         for (int r = 0; r < 16; ++r) x1[t][r] = b1p[(t * 16 + r) * 64 + l];
+    // W1's fragments stream from L2 kPD k-blocks ahead of their MFMAs (a ring of
+    // registers): at one or two waves per SIMD nothing else hides the L2 latency
+    constexpr int kPD = BGX_POLICY_W1_AHEAD;
+    uint4 wf[kPD + 1][2 * T];
+    #pragma unroll
+    for (int p = 0; p < kPD; ++p)
+        #pragma unroll
+        for (int f = 0; f < 2 * T; ++f) wf[p][f] = w1q[(p * 2 * T + f) * 64 + l];
+    #pragma unroll
     for (int kb = 0; kb < kKB1; ++kb) {
+        if (kb + kPD < kKB1) {
+            #pragma unroll
+            for (int f = 0; f < 2 * T; ++f) wf[(kb + kPD) % (kPD + 1)][f] = w1q[((kb + kPD) * 2 * T + f) * 64 + l];
+        }
+        __builtin_amdgcn_sched_barrier(0);
         const f16x8 bf = feats8(myrec, kb, h);         // exact in f16: no lo part
         #pragma unroll
         for (int t = 0; t < T; ++t) {
-            const f16x8 ah = as_h8(w1q[((kb * T + t) * 2 + 0) * 64 + l]);
-            const f16x8 al = as_h8(w1q[((kb * T + t) * 2 + 1) * 64 + l]);
+            const f16x8 ah = as_h8(wf[kb % (kPD + 1)][2 * t + 0]);
+            const f16x8 al = as_h8(wf[kb % (kPD + 1)][2 * t + 1]);
             x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bf, x1[t], 0, 0, 0);
             x1[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bf, x1[t], 0, 0, 0);
         }
@@ -624,6 +649,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
 }
 
+__global__ void k_counter_add(uint32_t* ctr, uint32_t v) {
+    if (threadIdx.x == 0) *ctr += v;
+}
+
 }  // namespace
 
 extern "C" {
@@ -647,9 +676,9 @@ int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const flo
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }
 
-int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packed, int32_t hidden, int32_t n_actions,
-                       uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out,
-                       float* value_out, float* logits_out, uint8_t* records_out, void* stream) {
+int bgx_policy_act_ctr(const uint8_t* records_dev, int32_t n, const float* packed, int32_t hidden, int32_t n_actions,
+                       uint64_t seed, uint32_t step, const uint32_t* step_ctr, int32_t greedy, int32_t* act_out,
+                       float* logp_out, float* value_out, float* logits_out, uint8_t* records_out, void* stream) {
     if (bgx_policy_packed_size(hidden, n_actions) < 0 || n < 0 || (n > 0 && (!records_dev || !packed || !act_out)))
         return BGX_EINVAL;
     if (n == 0) return BGX_OK;
@@ -668,11 +697,12 @@ int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packe
     do {                                                                                                      \
         if (plain)                                                                                            \
             hipLaunchKernelGGL((k_policy_act<TT, 0>), grid0, dim3(256), 0, s, records_dev, n, packed, n_actions, OT, \
-                               lo, hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out,   \
-                               skip ? 1 : 0);                                                                 \
+                               lo, hi, step, step_ctr, greedy, act_out, logp_out, value_out, logits_out,     \
+                               records_out, skip ? 1 : 0);                                                    \
         else                                                                                                  \
             hipLaunchKernelGGL((k_policy_act<TT, -1>), grid, blk, 0, s, records_dev, n, packed, n_actions, OT,   \
-                               lo, hi, step, greedy, act_out, logp_out, value_out, logits_out, records_out, 0); \
+                               lo, hi, step, step_ctr, greedy, act_out, logp_out, value_out, logits_out,     \
+                               records_out, 0);                                                               \
     } while (0)
     switch (T) {
         case 1: BGX_ACT(1); break;
@@ -681,6 +711,19 @@ int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packe
         default: BGX_ACT(4); break;
     }
 #undef BGX_ACT
+    return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
+}
+
+int bgx_policy_act_rec(const uint8_t* records_dev, int32_t n, const float* packed, int32_t hidden, int32_t n_actions,
+                       uint64_t seed, uint32_t step, int32_t greedy, int32_t* act_out, float* logp_out,
+                       float* value_out, float* logits_out, uint8_t* records_out, void* stream) {
+    return bgx_policy_act_ctr(records_dev, n, packed, hidden, n_actions, seed, step, nullptr, greedy, act_out, logp_out,
+                              value_out, logits_out, records_out, stream);
+}
+
+int bgx_counter_add(uint32_t* ctr_dev, uint32_t v, void* stream) {
+    if (!ctr_dev) return BGX_EINVAL;
+    hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(64), 0, (hipStream_t)stream, ctr_dev, v);
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }
 
