@@ -253,18 +253,24 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
     graph = None
     if S == 1 and graphs:
         try:
+            # the engine is joined before the capture and as its last call: a step
+            # leaves the next dispatch order on the engine's side stream, which a
+            # capture must not hold unjoined (hipErrorStreamCaptureUnjoined)
             cap = torch.cuda.Stream(dev)
             cap.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(cap):
+                engs[0].join()
                 for _ in range(2):
                     best, _ = one_ply(engs[0], vh)
                     engs[0].step(best, want_obs=False, want_info=False)
+                engs[0].join()
             torch.cuda.synchronize(dev)
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=cap):
                 for _ in range(2):
                     best, _ = one_ply(engs[0], vh)
                     engs[0].step(best, want_obs=False, want_info=False)
+                engs[0].join()
             torch.cuda.synchronize(dev)
         except Exception as ex:                        # eager launches then
             print(f"[bench] C2 graph capture failed ({ex}); eager", file=sys.stderr)

@@ -213,7 +213,10 @@ __device__ __forceinline__ bool table_insert(SlotPtr tab, uint32_t a, uint32_t b
         }
         base += 64u;
     }
-    return false;
+    // exhausted (unreachable under the 7/8 cap): report "inserted" without a
+    // slot, so the caller's n_unique reaches cap_unique and the walk overflows
+    // to the next tier instead of dropping the entry as a duplicate
+    return true;
 }
 
 // Per-lane (divergent) membership test along the same linear probe sequence.
@@ -259,8 +262,11 @@ __device__ __forceinline__ bool probe_lane(SlotPtr tab, uint32_t a, uint32_t b, 
         }
         h = (h + 4u) & mask;
     }
+    // exhausted (unreachable under the 7/8 cap): "absent", so the caller's fill
+    // check (commit: fill() + n >= cap_unique; memo_batch: no room) overflows the
+    // walk or leaves the state unrecorded -- never a silently dropped entry
     slot = h;
-    return true;
+    return false;
 }
 
 // Insert the keys of the lanes in `fresh`, each lane's `slot` from probe_lane
