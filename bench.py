@@ -323,6 +323,12 @@ def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
     nt = (hidden + 15) // 16
     # k_eval (the MFMA kernel): algorithmic FLOPs of its leaves / its HIP-event time
     eval_tflops = leaves * flop_per_leaf / (eval_ms / batches * 1e-3) / batches / 1e12 if eval_ms > 0 else None
+    # evaluator tile forms: narrow = 16 units (hi + lo rows) per 32-row tile,
+    # wide (nt > 4) = 32 units per tile with hi and lo as two k-blocks of one accumulator
+    wide = nt > 4
+    units = 32 * ((nt + 1) // 2) if wide else 16 * nt
+    tiles = (f"H as {(nt + 1) // 2} 32-unit tiles, hi and lo as two k-blocks" if wide
+             else f"H as {nt} 16-unit hi+lo tiles")
     return {"config": f"C4: B={eng.batch} roots/GPU, 2-ply expectimax over 21 rolls, value MLP 198->{hidden}->1 "
                       "(W1 split hi+lo on f16 MFMA, exact f16 features; fp32-equivalent); leaves encoded with "
                       "the root mover's one-hot, min over replies",
@@ -335,10 +341,9 @@ def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
                          "bound": "mfma", "achieved": eval_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": eval_tflops / BF16_PEAK_TFLOPS if eval_tflops else None,
                          "flop_per_leaf": flop_per_leaf,
-                         "issued_over_algorithmic": 2 * (16 * nt / hidden) * (208 / 198),
-                         "note": f"issued MFMA work = algorithmic x 2 (W1 hi+lo rows for fp32 accuracy) x "
-                                 f"{16 * nt}/{hidden} (H as {nt} 16-unit hi+lo tiles) x 208/198 (K padding, bias "
-                                 "as a feature)"}}
+                         "issued_over_algorithmic": 2 * (units / hidden) * (208 / 198),
+                         "note": f"issued MFMA work = algorithmic x 2 (W1 hi+lo for fp32 accuracy) x "
+                                 f"{units}/{hidden} ({tiles}) x 208/198 (K padding, bias as a feature)"}}
 
 
 def issue_roofline(sq: dict, lanes: int, kern_ms: float, src) -> dict:

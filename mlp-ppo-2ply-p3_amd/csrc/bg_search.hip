@@ -53,14 +53,8 @@ using namespace bg;
 #ifndef BGX_EVAL_SKIP
 #define BGX_EVAL_SKIP 0
 #endif
-#ifndef BGX_EVAL_G
-#define BGX_EVAL_G 4
-#endif
 #ifndef BGX_EVAL_NARROW_WAVES
 #define BGX_EVAL_NARROW_WAVES 4
-#endif
-#ifndef BGX_EVAL_SINGLE_MIN_NT
-#define BGX_EVAL_SINGLE_MIN_NT 99
 #endif
 
 namespace {
@@ -92,18 +86,26 @@ __device__ __forceinline__ int nd_roll(int k) {     // k-th non-doubles roll ind
 }
 
 // Value net packed for MFMA (bgx_value_pack), in floats (H <= 128):
-//                         hdr [4] (e1 as int bits), then NT = ceil(H/16) tiles of
-//                         16 hidden units with their hi AND lo parts in one 32-row
-//                         MFMA tile (row m: unit 16t + (m&7) + 8(m>>4), part (m>>3)&1):
+//                         hdr [4] (e1 as int bits), then NT = ceil(H/16) 16-unit
+//                         slices.  Narrow form (NT <= 4): NT tiles of 16 hidden units
+//                         with their hi AND lo parts in one 32-row MFMA tile (row m:
+//                         unit 16t + (m&7) + 8(m>>4), part (m>>3)&1):
 //     w1q [13][NT][64] x uint4   lane l: the 8 f16 of row l&31 at k = kperm(kb, l>>5, i),
 //                                i = 0..7, of W1s = [W1 | b1] * 2^e1 (the two `off`
 //                                columns divided by 15; b1 rides a constant-1 feature)
 //     wvq [NT][8][64] f32        value_head.weight[unit(t, j, l)] * 2^-e1 for the
 //                                accumulator pair (r, r+4), r = j < 4 ? j : j + 4
+//                         Wide form (NT > 4): NW = ceil(NT/2) tiles of 32 units, the
+//                         hi and lo parts as two k-blocks of the same accumulator:
+//     w1q [13][NW][2][64] x uint4  lane l: row unit 32T + (l&31), part 0 = hi, 1 = lo
+//     wvq [NW][4][64][4] f32     value_head.weight[32T + 8(r>>2) + 4(l>>5) + (r&3)] * 2^-e1
+//                                for accumulator register r of lane l (at [T][r>>2][l][r&3])
 // The features are then exact small integers / halves in f16, so one hi and one
-// lo MFMA product give fp32-grade accuracy, and hi + lo of a unit are summed
-// from two accumulator registers of the same lane.
-__host__ __device__ inline int sz_f16(int NT) { return 4 + kKB * NT * 64 * 4 + NT * 8 * 64; }
+// lo MFMA product give fp32-grade accuracy: narrow, hi + lo of a unit are summed
+// from two accumulator registers of the same lane; wide, the accumulator sums them.
+__host__ __device__ constexpr bool wide_tiles(int NT) { return NT > 4; }
+__host__ __device__ constexpr int slices(int NT) { return wide_tiles(NT) ? (NT + 1) & ~1 : NT; }
+__host__ __device__ inline int sz_f16(int NT) { return 4 + kKB * slices(NT) * 64 * 4 + slices(NT) * 8 * 64; }
 
 constexpr int kFeatBias = -2;
 // Permuted K order of the f16 section: k-blocks 0-5 = P1 points, 6-11 = P2 points;
@@ -644,33 +646,25 @@ __device__ __forceinline__ uint32_t f16_pair(uint32_t ab, float s0, float s1) {
     return __builtin_bit_cast(uint32_t, r);
 }
 
-// packed u16x2 ops (clang scalarises them from vector code into cmp/cndmask pairs)
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-    uint32_t r;
-    __asm__("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b) {
-    uint32_t r;
-    __asm__("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ uint32_t pk_mul_lo_u16(uint32_t a, uint32_t b) {
-    uint32_t r;
-    __asm__("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
 // the four units of two points with counts (a, b) (immutable_board.py:180-195) as
-// f16 pairs [u_k(a), u_k(b)], k = 0..3: n>=1, n>=2, n>=3, (n-3)/2 if n>=3
+// f16 pairs [u_k(a), u_k(b)], k = 0..3: n>=1, n>=2, n>=3, (n-3)/2 if n>=3.
+// t = (1024 + a, 1024 + b) in f16 (unit spacing there, so every step is exact):
+// u_k = clamp01(t - 1024 - k) for k < 3 (the VOP3P clamp bit), u_3 = max(t/2 - 513.5, 0).
+// One asm block: its outputs feed MFMA operands, and hipcc's hazard recognizer does
+// not see inside inline asm, so the VALU-write -> MFMA-read wait states (s_nop 1)
+// end the string.
 __device__ __forceinline__ uint4 units_pair(uint32_t byte) {
-    const uint32_t x = (byte & 15u) | ((byte & 0xF0u) << 12);
-    const uint32_t one = 0x00010001u, f1 = 0x3C003C00u;
-    const uint32_t x1 = pk_subsat_u16(x, one), x2 = pk_subsat_u16(x1, one), x3 = pk_subsat_u16(x2, one);
-    const uint32_t u0 = pk_mul_lo_u16(pk_min_u16(x, one), f1);
-    const uint32_t u1 = pk_mul_lo_u16(pk_min_u16(x1, one), f1);
-    const uint32_t u2 = pk_mul_lo_u16(pk_min_u16(x2, one), f1);
-    return make_uint4(u0, u1, u2, f16_pair(x3, 0.5f, 0.5f));
+    const uint32_t t = (byte & 15u) | ((byte & 0xF0u) << 12) | 0x64006400u;
+    uint32_t u0, u1, u2, u3;
+    __asm__("v_pk_add_f16 %0, %4, %5 clamp\n\t"
+            "v_pk_add_f16 %1, %4, %6 clamp\n\t"
+            "v_pk_add_f16 %2, %4, %7 clamp\n\t"
+            "v_pk_fma_f16 %3, %4, %8, %9\n\t"
+            "v_pk_max_f16 %3, %3, 0\n\t"
+            "s_nop 1"
+            : "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3)
+            : "v"(t), "s"(0xE400E400u), "s"(0xE401E401u), "s"(0xE402E402u), "s"(0x38003800u), "v"(0xE003E003u));
+    return make_uint4(u0, u1, u2, u3);
 }
 
 // the two point counts (nibbles) k-block kb < 12 takes from this lane's half h:
@@ -711,9 +705,56 @@ __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0
 // accumulated per pass (2 x 4 x 16 accumulator VGPRs); H = 128 takes two passes
 // over K, regenerating the features.  `z` = an opaque zero offset that keeps the
 // LDS fragment reads inside the loops.
+// relu as one v_max_i32 on the float's bits (a negative float is a negative int;
+// fmaxf would first canonicalize the MFMA result with a second v_max_f32, and inline
+// asm would hide the MFMA-result read from the hazard recognizer, which must pad it)
+__device__ __forceinline__ float relu_raw(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
+template <int NT>
+__device__ __forceinline__ void eval_leaves_wide(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z,
+                                                 float bias, float (&v)[2]) {
+    constexpr int NW = slices(NT) / 2;
+    const int l = lane_id(), h = l >> 5;
+    f32x16 x[2][NW];
+    #pragma unroll
+    for (int kb = 0; kb < kKB; ++kb) {
+        const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
+        #pragma unroll
+        for (int t = 0; t < NW; ++t) {
+            const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 0) * 64 + l + z]);
+            const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 1) * 64 + l + z]);
+            x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, kb == 0 ? (f32x16){} : x[0][t], 0, 0, 0);
+            x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f1, kb == 0 ? (f32x16){} : x[1][t], 0, 0, 0);
+            x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f0, x[0][t], 0, 0, 0);
+            x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f1, x[1][t], 0, 0, 0);
+        }
+    }
+    // value head: relu times the head weights, 4 registers' weights per ds_read_b128
+    float a[2] = {0.0f, 0.0f};
+    #pragma unroll
+    for (int t = 0; t < NW; ++t)
+        #pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+            const float4 w = reinterpret_cast<const float4*>(wvs)[(t * 4 + r4) * 64 + l + z];
+            #pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 0]), w.x, a[n]);
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 1]), w.y, a[n]);
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 2]), w.z, a[n]);
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 3]), w.w, a[n]);
+            }
+        }
+    #pragma unroll
+    for (int n = 0; n < 2; ++n) v[n] = a[n] + __shfl_xor(a[n], 32) + bias;
+}
+
 template <int NT>
 __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z, float bias,
                                             float (&v)[2]) {
+    if constexpr (wide_tiles(NT)) {
+        eval_leaves_wide<NT>(wq, wvs, L, z, bias, v);
+        return;
+    }
     constexpr int G = NT < 4 ? NT : 4;
     const int l = lane_id(), h = l >> 5;
     v[0] = 0.0f;
@@ -800,52 +841,17 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
     for (int n = 0; n < 2; ++n) v[n] += __shfl_xor(v[n], 32) + bias;
 }
 
-// H > 64 (NT > 4 unit tiles): one 32-leaf tile at a time with ALL unit tiles'
-// accumulators live (NT x 16 VGPRs), so each k-block's features are generated once
-// (the two-tile form regenerated them in a second pass over K: twice the VALU feature
-// work, which kept the MFMA pipe ~half idle at H = 128).  The weight fragments are
-// read once per 32 leaves instead of once per 64 (one ds_read_b128 per MFMA).
-template <int NT, int G>
-__device__ __forceinline__ float eval_leaf_tile(const uint4* wq, const float* wvs, const Leaf& L, int z, float bias) {
-    const int l = lane_id(), h = l >> 5;
-    float v = 0.0f;
-    #pragma unroll 1
-    for (int g0 = 0; g0 < NT; g0 += G) {
-        f32x16 x[G];
-        #pragma unroll
-        for (int kb = 0; kb < kKB; ++kb) {
-            const f16x8 f = feat16(L, kb, h);
-            #pragma unroll
-            for (int t = 0; t < G; ++t) {
-                const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + g0 + t) * 64 + l + z]);
-                x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
-            }
-        }
-        #pragma unroll
-        for (int t = 0; t < G; ++t)
-            #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int r = j < 4 ? j : j + 4;
-                v = fmaf(fmaxf(x[t][r] + x[t][r + 4], 0.0f), wvs[((g0 + t) * 8 + j) * 64 + l + z], v);
-            }
-    }
-    return v + __shfl_xor(v, 32) + bias;
-}
-
 // workgroup shape of the evaluators: 4 waves (NT <= 4: <= 52 KiB of weights in LDS,
 // several workgroups per CU) or 8 waves (H = 128: 120 KiB, one workgroup per CU,
 // two waves per SIMD)
-constexpr int kEvalG = BGX_EVAL_G;           // unit tiles accumulated per pass (single-tile form)
 template <int NT> struct EvalShape {
     static constexpr int kWaves = NT <= 4 ? BGX_EVAL_NARROW_WAVES : BGX_EVAL_WIDE_WAVES;
-    static constexpr bool kSingle = NT >= BGX_EVAL_SINGLE_MIN_NT;   // one 32-leaf tile per call
-    static constexpr int kG = NT < kEvalG ? NT : kEvalG;
 };
 
 template <int NT>
 __device__ __forceinline__ void stage_weights(uint4* wq, float* wvs, const uint4* w1q, const float* wvq) {
-    for (int i = threadIdx.x; i < kKB * NT * 64; i += blockDim.x) wq[i] = w1q[i];
-    for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = wvq[i];
+    for (int i = threadIdx.x; i < kKB * slices(NT) * 64; i += blockDim.x) wq[i] = w1q[i];
+    for (int i = threadIdx.x; i < slices(NT) * 8 * 64; i += blockDim.x) wvs[i] = wvq[i];
     __syncthreads();
 }
 
@@ -858,8 +864,8 @@ template <int NT>
 __global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) __attribute__((amdgpu_waves_per_eu(NT <= 4 ? 3 : 2)))
 void k_eval(EvalArgs E) {
     constexpr int W = EvalShape<NT>::kWaves;
-    __shared__ uint4 wq[kKB * NT * 64];
-    __shared__ float wvs[NT * 8 * 64];
+    __shared__ uint4 wq[kKB * slices(NT) * 64];
+    __shared__ float wvs[slices(NT) * 8 * 64];
     const int l = lane_id(), h = l >> 5, c = l & 31;
     stage_weights<NT>(wq, wvs, E.w1q, E.wvq);
     const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
@@ -881,16 +887,7 @@ void k_eval(EvalArgs E) {
         #pragma unroll
         for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
         float v[2];
-        if (EvalShape<NT>::kSingle) {
-            // the second tile's weight reads depend on the first tile's value (an opaque
-            // zero offset): LLVM cannot interleave the two 128-accumulator chains
-            v[0] = eval_leaf_tile<NT, EvalShape<NT>::kG>(wq, wvs, L[0], z, E.bv);
-            int z2 = z;
-            __asm__ volatile("" : "+s"(z2) : "v"(v[0]));
-            v[1] = eval_leaf_tile<NT, EvalShape<NT>::kG>(wq, wvs, L[1], z2, E.bv);
-        } else {
-            eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
-        }
+        eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
         #pragma unroll
         for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
         #pragma unroll
@@ -925,8 +922,8 @@ struct EvalRowsArgs {
 template <int NT>
 __global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) void k_eval_rows(EvalRowsArgs E) {
     constexpr int W = EvalShape<NT>::kWaves;
-    __shared__ uint4 wq[kKB * NT * 64];
-    __shared__ float wvs[NT * 8 * 64];
+    __shared__ uint4 wq[kKB * slices(NT) * 64];
+    __shared__ float wvs[slices(NT) * 8 * 64];
     const int l = lane_id(), h = l >> 5, c = l & 31;
     stage_weights<NT>(wq, wvs, E.w1q, E.wvq);
     const long long rows = *E.nrows;
@@ -1025,10 +1022,14 @@ __global__ __launch_bounds__(1024) void k_value_pack16(const float* W1, const fl
         e1 = e1 < -100 ? -100 : (e1 > 100 ? 100 : e1);
     }
     if (tid == 0) { hdr[0] = e1; hdr[1] = 0; hdr[2] = 0; hdr[3] = 0; }
-    const int n = kKB * NT * 64 * 8;
+    const bool wide = wide_tiles(NT);
+    const int NS = slices(NT);              // 64-lane uint4 fragments per k-block
+    const int n = kKB * NS * 64 * 8;
     for (int idx = tid; idx < n; idx += 1024) {
-        const int i = idx & 7, l = (idx >> 3) & 63, t = (idx >> 9) % NT, kb = (idx >> 9) / NT;
-        const int m = l & 31, unit = 16 * t + (m & 7) + 8 * (m >> 4), part = (m >> 3) & 1;
+        const int i = idx & 7, l = (idx >> 3) & 63, t = (idx >> 9) % NS, kb = (idx >> 9) / NS;
+        const int m = l & 31;
+        const int unit = wide ? 32 * (t >> 1) + m : 16 * t + (m & 7) + 8 * (m >> 4);
+        const int part = wide ? (t & 1) : (m >> 3) & 1;
         const int f = kperm(kb, l >> 5, i);
         float w = 0.0f;
         if (unit < H) {
@@ -1037,11 +1038,18 @@ __global__ __launch_bounds__(1024) void k_value_pack16(const float* W1, const fl
         }
         _Float16 hi, lo;
         split16(ldexpf(w, e1), hi, lo);
-        w1q[((size_t)(kb * NT + t) * 64 + l) * 8 + i] = part ? lo : hi;
+        w1q[((size_t)(kb * NS + t) * 64 + l) * 8 + i] = part ? lo : hi;
     }
-    for (int idx = tid; idx < NT * 8 * 64; idx += 1024) {
-        const int l = idx & 63, j = (idx >> 6) & 7, t = idx >> 9;
-        const int unit = 16 * t + (j & 3) + 8 * (j >> 2) + 4 * (l >> 5);
+    for (int idx = tid; idx < NS * 8 * 64; idx += 1024) {
+        const int l = idx & 63;
+        int unit;
+        if (wide) {
+            const int lw = (idx >> 2) & 63, r = (idx & 3) + 4 * ((idx >> 8) & 3), T = idx >> 10;
+            unit = 32 * T + 8 * (r >> 2) + 4 * (lw >> 5) + (r & 3);
+        } else {
+            const int j = (idx >> 6) & 7, t = idx >> 9;
+            unit = 16 * t + (j & 3) + 8 * (j >> 2) + 4 * (l >> 5);
+        }
         wvq[idx] = unit < H ? ldexpf(wv[unit], -e1) : 0.0f;
     }
 }
@@ -1144,7 +1152,7 @@ int bgx_value_pack(const float* W1, const float* b1, const float* wv, const floa
     if (total < 0 || !W1 || !b1 || !wv || !bv || !packed) return BGX_EINVAL;
     const int NT = value_tiles16(hidden);
     hipLaunchKernelGGL(k_value_pack16, dim3(1), dim3(1024), 0, (hipStream_t)stream, W1, b1, wv, hidden, NT,
-                       (int*)packed, (_Float16*)(packed + 4), packed + 4 + kKB * NT * 64 * 4);
+                       (int*)packed, (_Float16*)(packed + 4), packed + 4 + kKB * slices(NT) * 64 * 4);
     SCK(hipGetLastError());
     return BGX_OK;
 }
@@ -1183,7 +1191,7 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     hipLaunchKernelGGL(k_rows, dim3((unsigned)gr), dim3(256), 0, s, A, row_lane, lane_off, total, nullptr, rowside,
                        rowkey);
     const EvalRowsFn kr = eval_rows_kernel(NT);
-    const EvalRowsArgs E{rowkey, rowside, total, vrow, (const uint4*)(vpacked + 4), vpacked + 4 + kKB * NT * 64 * 4,
+    const EvalRowsArgs E{rowkey, rowside, total, vrow, (const uint4*)(vpacked + 4), vpacked + 4 + kKB * slices(NT) * 64 * 4,
                          value_bias};
     hipLaunchKernelGGL(kr, dim3(eval_grid(e, kr, NT)), dim3(64 * eval_waves(NT)), 0, s, E);
     hipLaunchKernelGGL(k_one_ply_reduce, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, vrow, best_out,
@@ -1297,7 +1305,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const int NT = value_tiles16(hidden);
         const float* f16s = vpacked;
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
-                   (const uint4*)(f16s + 4), f16s + 4 + kKB * NT * 64 * 4, value_bias};
+                   (const uint4*)(f16s + 4), f16s + 4 + kKB * slices(NT) * 64 * 4, value_bias};
         // the non-doubles enumerator: the row-level walk held to 80 VGPRs (6 waves/SIMD,
         // +1.2 % over its natural 91).  A/B: BGX_2PLY_ROWS=0 the per-job walk only;
         // BGX_2PLY_LWPE=1 the row-level walk without the floor, =8 the per-job walk
