@@ -45,9 +45,10 @@ class PolicyNet(nn.Module):
 
     # ---------------------------------------------------- HIP fast path --
     @torch.no_grad()
-    def pack(self) -> torch.Tensor:
+    def pack(self, inplace: bool = False) -> torch.Tensor:
         """Pack the weights into the MFMA operand layout of bgx_policy_act (call
-        after every optimizer step)."""
+        after every optimizer step).  `inplace`: rewrite the previous pack's buffer
+        (its address is baked into captured HIP graphs of act)."""
         L = _lib.load()
         H, A = self.fc1.out_features, self.action_head.out_features
         n = L.bgx_policy_packed_size(H, A)
@@ -57,7 +58,11 @@ class PolicyNet(nn.Module):
         ps = [t.detach().float().contiguous() for t in (self.fc1.weight, self.fc1.bias, self.action_head.weight,
                                                          self.action_head.bias, self.value_head.weight,
                                                          self.value_head.bias)]
-        out = torch.empty(n, dtype=torch.float32, device=dev)
+        prev = getattr(self, "_packed", None)
+        if inplace and prev is not None and prev.numel() == n and prev.device == dev:
+            out = prev
+        else:
+            out = torch.empty(n, dtype=torch.float32, device=dev)
         s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         check(L.bgx_policy_pack(*[_ptr(t) for t in ps], H, A, _ptr(out), s), "bgx_policy_pack")
         self._packed = out

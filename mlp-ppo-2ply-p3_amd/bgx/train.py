@@ -473,7 +473,7 @@ class PPOTrainer:
     def __init__(self, batch: int = 65536, horizon: int = 64, hidden: int = 128, n_actions: int = 500,
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
                  chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True,
-                 entropy_anneal: str = "train"):
+                 entropy_anneal: str = "train", shards: int | None = None, graphs: bool | None = None):
         if entropy_anneal not in ("train", "train_single"):
             raise ValueError(f"entropy_anneal must be 'train' or 'train_single', got {entropy_anneal!r}")
         self.entropy_anneal = entropy_anneal
@@ -485,8 +485,23 @@ class PPOTrainer:
         self.chunk = chunk
         self.fused = (self.dev.type == "cuda") if fused is None else fused
         self.amp = amp            # the reference's autocast (fp16 on the GPU); False = fp32 update
-        self.eng = Engine(batch=batch, max_moves=n_actions, seed=seed * 1_000_003 + self.rank, dice="philox",
-                          auto_reset=True, device=self.dev)
+        # the B lanes as S engines on S streams (bench.py's C3 layout: one shard's policy
+        # kernel runs beside the other's env step); shard 0 keeps the 1-shard seeds
+        if shards is None:
+            shards = 2 if self.dev.type == "cuda" and batch >= 32768 and batch % 256 == 0 else 1
+        if batch % shards:
+            raise ValueError(f"batch {batch} is not a multiple of shards {shards}")
+        self.S = shards
+        self.engs = [Engine(batch=batch // shards, max_moves=n_actions,
+                            seed=seed * 1_000_003 + self.rank + 7_919 * k, dice="philox", auto_reset=True,
+                            device=self.dev) for k in range(shards)]
+        self.eng = self.engs[0]
+        # rollout steps replayed as HIP graphs (2 steps per graph, one graph per slot pair
+        # and shard), captured at the end of the first rollout: the engines' host state is
+        # then a 2-step fixed point (bench.py C3).  Equal to the eager rollout
+        # (tests/test_gpu_train.py::test_rollout_graphs_match_eager).
+        self.graphs = (self.dev.type == "cuda" and horizon % 2 == 0 and not pinned) if graphs is None else graphs
+        self._graphs = None
         torch.manual_seed(seed)
         self.net = PolicyNet(hidden_size=hidden, action_size=n_actions).to(self.dev)
         if _world(process_group) > 1:
@@ -516,24 +531,82 @@ class PPOTrainer:
             self.copy_stream = torch.cuda.Stream(self.dev)
         self.ep_carry = torch.zeros(B, dtype=torch.float64, **kw)     # train.py:58 episode_rewards
         self.last_episode_stats = None
-        self.eng.reset(want_obs=False)
+        for e in self.engs:
+            e.reset(want_obs=False)
+        self._streams = ([torch.cuda.current_stream(self.dev)] + [torch.cuda.Stream(self.dev) for _ in range(self.S - 1)]
+                         if self.dev.type == "cuda" else [None])
+
+    def _slot(self, k: int, t: int):
+        """Shard k's views of rollout slot t (contiguous row ranges)."""
+        n = self.B // self.S
+        lo, hi = k * n, (k + 1) * n
+        b = self.buf
+        return ((b["actions"][t][lo:hi], b["logp"][t][lo:hi], b["values"][t][lo:hi]), b["records"][t][lo:hi],
+                (b["rewards"][t][lo:hi], b["dones"][t][lo:hi]))
+
+    def _act_step(self, k: int, t: int, step: int, step_ctr=None):
+        out, rec, env_out = self._slot(k, t)
+        self.net.act(self.engs[k], seed=self.seed * 7919 + self.rank + 104_729 * k, step=step, step_ctr=step_ctr,
+                     out=out, records_out=rec)
+        self.engs[k].step(out[0], want_obs=False, want_info=False, out=env_out)
+
+    def _capture(self):
+        """One graph per (slot pair, shard): act + step for slots t and t + 1 with the
+        noise step read from the shard's device counter (advanced by 2 per replay),
+        the engine joined at the end (its side-stream dispatch order)."""
+        self._ctrs = [torch.zeros(1, dtype=torch.int32, device=self.dev) for _ in range(self.S)]
+        caps = [torch.cuda.Stream(self.dev) for _ in range(self.S)]
+        for k in range(self.S):
+            caps[k].wait_stream(self._streams[k])
+            with torch.cuda.stream(caps[k]):
+                self.engs[k].join()
+        torch.cuda.synchronize(self.dev)
+        graphs = []
+        for t in range(0, self.T, 2):
+            row = []
+            for k in range(self.S):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=caps[k]):
+                    for j in range(2):
+                        self._act_step(k, t + j, j, self._ctrs[k])
+                    self.engs[k].join()
+                    PolicyNet.advance_counter(self._ctrs[k], 2)
+                row.append(g)
+            graphs.append(row)
+        torch.cuda.synchronize(self.dev)
+        self._graphs = graphs
 
     def rollout(self):
         """T env steps on all B lanes (train.py:46-99 without the Python loops)."""
-        self.net.pack()
+        self.net.pack(inplace=True)
         buf = self.buf
-        for t in range(self.T):
-            self.net.act(self.eng, seed=self.seed * 7919 + self.rank, step=self.step_counter,
-                         out=(buf["actions"][t], buf["logp"][t], buf["values"][t]), records_out=buf["records"][t])
+        cur = self._streams[0]
+        for st in self._streams[1:]:
+            st.wait_stream(cur)                  # the packed weights, the previous update
+        if self._graphs is not None:
+            for k in range(self.S):
+                with torch.cuda.stream(self._streams[k]):
+                    self._ctrs[k].fill_(self.step_counter)
+            for row in self._graphs:             # the shards' replays side by side
+                for k in range(self.S):
+                    with torch.cuda.stream(self._streams[k]):
+                        row[k].replay()
+            self.step_counter += self.T
+        for t in range(self.T if self._graphs is None else 0):
+            for k in range(self.S):
+                with torch.cuda.stream(self._streams[k]):
+                    self._act_step(k, t, self.step_counter)
             self.step_counter += 1
-            self.eng.step(buf["actions"][t], want_obs=False, want_info=False,
-                          out=(buf["rewards"][t], buf["dones"][t]))
             if self.pinned is not None:
-                cur = torch.cuda.current_stream(self.dev)
-                self.copy_stream.wait_stream(cur)
+                for st in self._streams:
+                    self.copy_stream.wait_stream(st)
                 with torch.cuda.stream(self.copy_stream):
                     for k in buf:
                         self.pinned[k][t].copy_(buf[k][t], non_blocking=True)
+        for st in self._streams[1:]:
+            cur.wait_stream(st)
+        if self.graphs and self._graphs is None:
+            self._capture()
         st = episode_stats(buf["rewards"], buf["dones"], buf["records"][:, :, 52], self.ep_carry)
         if _world(self.group) > 1:
             dist.all_reduce(st, group=self.group)

@@ -509,6 +509,7 @@ static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, c
     if (e->memo_mode == 2 && e->lds_log == 8) { STEP_K(0, 8, 2); return; }
     if (e->memo_mode == 0) {
         if (e->lds_log == 8) STEP_K(0, 8, 0);
+        else if (e->heavy_wpe == 4) STEP_K(0, 9, 0, false, 4);
         else STEP_K(0, 9, 0);
         return;
     }

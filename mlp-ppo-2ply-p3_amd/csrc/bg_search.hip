@@ -1313,6 +1313,8 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const char* lw = getenv("BGX_2PLY_LWPE");
         const char* rw = getenv("BGX_2PLY_ROWS");
         void (*klight)(S2) = lw && atoi(lw) == 8 ? k_enum<kLogLight, -1, 0, 8>
+                             : lw && atoi(lw) == 7 ? k_enum<kLogLight, -1, 3, 7>
+                             : lw && atoi(lw) == 9 ? k_enum<kLogLight, -1, 3, 8>
                              : (rw && rw[0] == '0') ? k_enum<kLogLight, -1, 0, 1>
                              : (lw && atoi(lw) == 1) ? k_enum<kLogLight, -1, 3, 1> : k_enum<kLogLight, -1, 3, 6>;
         int g_light = persistent_grid(e, klight, 32);

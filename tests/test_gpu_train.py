@@ -215,3 +215,24 @@ def test_fc1_from_records_matches_autocast_gemm(hidden):
     assert float((h == blas).float().mean()) > 0.99
     # bad arguments are refused, not run
     assert L.bgx_fc1_packed_size(130) < 0 and L.bgx_fc1_packed_size(42) < 0
+
+
+def test_rollout_graphs_match_eager():
+    """The trainer's rollout as HIP graphs (2 steps per graph per shard, captured at the
+    end of the first rollout, the noise step from a device counter) fills the same
+    buffers as the eager rollout, rollout after rollout, with 2 shards on 2 streams."""
+    from bgx.train import PPOTrainer
+    trs = [PPOTrainer(batch=32768, horizon=4, seed=7, shards=2, graphs=g) for g in (False, True)]
+    assert trs[1].S == 2
+    for it in range(3):
+        for tr in trs:
+            tr.rollout()
+        torch.cuda.synchronize()
+        assert (trs[1]._graphs is not None) and trs[0]._graphs is None
+        for k in trs[0].buf:
+            assert torch.equal(trs[0].buf[k], trs[1].buf[k]), (it, k)
+        assert trs[0].step_counter == trs[1].step_counter == 4 * (it + 1)
+    # the two shards draw different games and noise
+    a = trs[0].buf["records"][:, :16384]
+    b = trs[0].buf["records"][:, 16384:]
+    assert not torch.equal(a, b)
