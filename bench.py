@@ -266,7 +266,7 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
                 engs[0].join()
             torch.cuda.synchronize(dev)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=cap):
+            with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
                 for _ in range(2):
                     best, _ = one_ply(engs[0], vh)
                     engs[0].step(best, want_obs=False, want_info=False)
@@ -497,7 +497,7 @@ def main():
                 row = []
                 for k in range(S):
                     e, b, gr = engs[k], bufs[k], torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gr, stream=caps[k]):
+                    with torch.cuda.graph(gr, stream=caps[k], capture_error_mode="thread_local"):
                         for i in range(g0, g0 + G):
                             net.act(e, seed=4242 + rank * 16 + k, step=i, step_ctr=ctrs[k],
                                     out=(b["act"][i], b["logp"][i], b["value"][i]), records_out=b["records"][i])

@@ -553,7 +553,8 @@ class PPOTrainer:
     def _capture(self):
         """One graph per (slot pair, shard): act + step for slots t and t + 1 with the
         noise step read from the shard's device counter (advanced by 2 per replay),
-        the engine joined at the end (its side-stream dispatch order)."""
+        the engine joined at the end (its side-stream dispatch order).  Thread-local
+        capture mode: a communicator's watchdog thread may query events meanwhile."""
         self._ctrs = [torch.zeros(1, dtype=torch.int32, device=self.dev) for _ in range(self.S)]
         caps = [torch.cuda.Stream(self.dev) for _ in range(self.S)]
         for k in range(self.S):
@@ -566,7 +567,7 @@ class PPOTrainer:
             row = []
             for k in range(self.S):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=caps[k]):
+                with torch.cuda.graph(g, stream=caps[k], capture_error_mode="thread_local"):
                     for j in range(2):
                         self._act_step(k, t + j, j, self._ctrs[k])
                     self.engs[k].join()
@@ -606,7 +607,12 @@ class PPOTrainer:
         for st in self._streams[1:]:
             cur.wait_stream(st)
         if self.graphs and self._graphs is None:
-            self._capture()
+            try:
+                self._capture()
+            except RuntimeError as ex:           # eager rollouts then (same results)
+                torch.cuda.synchronize(self.dev)
+                print(f"[bgx] rollout graph capture failed ({ex}); eager rollouts", flush=True)
+                self.graphs, self._graphs = False, None
         st = episode_stats(buf["rewards"], buf["dones"], buf["records"][:, :, 52], self.ep_carry)
         if _world(self.group) > 1:
             dist.all_reduce(st, group=self.group)
