@@ -95,6 +95,9 @@ def launch_ranks(n: int) -> int:
 
 
 def dist_init(gpus: int):
+    """One process per GPU.  BGX_DIST_FORCE=1 (tests) initialises the process group
+    even at WORLD_SIZE=1, so RCCL's init, all-reduce, all-gather and barrier, and
+    the HIP-graph captures beside its watchdog thread, run on a one-GPU box."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if ws != gpus:
@@ -106,36 +109,47 @@ def dist_init(gpus: int):
                          "(BGX_DIST_BACKEND=gloo rehearses several ranks on one GPU)")
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(ndev, 1)
     torch.cuda.set_device(local)
-    if ws > 1:
+    if ws > 1 or os.environ.get("BGX_DIST_FORCE") == "1":
         import torch.distributed as dist
+        if ws == 1:                                 # a one-rank group: rendezvous on this host
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         # "nccl" is RCCL on ROCm (one rank per GPU); BGX_DIST_BACKEND=gloo lets
         # several ranks share one GPU for functional rehearsals of the N>1 path
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    return rank, ws, local, backend if ws > 1 else None
+        return rank, ws, local, backend
+    return rank, ws, local, None
+
+
+def _dist_on() -> bool:
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
 
 
 def gather_ranks(x, ws: int) -> list:
     """Every rank's list of floats, in rank order (a CUDA tensor: RCCL and gloo)."""
-    t = torch.tensor(x, dtype=torch.float64, device="cuda")
-    if ws == 1:
+    if not _dist_on():
         return [x]
     import torch.distributed as dist
+    t = torch.tensor(x, dtype=torch.float64, device="cuda")
     out = [torch.empty_like(t) for _ in range(ws)]
     dist.all_gather(out, t)
     return [o.tolist() for o in out]
 
 
 def barrier(ws):
-    if ws > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.barrier()
 
 
 def max_over_ranks(x: float, ws: int) -> float:
-    if ws == 1:
+    if not _dist_on():
         return x
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
@@ -144,7 +158,7 @@ def max_over_ranks(x: float, ws: int) -> float:
 
 
 def sum_over_ranks(x: float, ws: int) -> float:
-    if ws == 1:
+    if not _dist_on():
         return x
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
@@ -204,7 +218,7 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4):
            "ranks": ws, "env_steps_per_s_incl_update": steps / el, "seconds_per_iteration": el / iters,
            "rollout_s": sum(m["rollout_s"] for m in ms) / iters, "update_s": sum(m["update_s"] for m in ms) / iters,
            "losses_last": {k: ms[-1][k] for k in ("policy_loss", "value_loss", "entropy", "total_loss")}}
-    if ws > 1:      # data parallel: the all-reduced update leaves every rank on the same weights
+    if _dist_on():  # data parallel: the all-reduced update leaves every rank on the same weights
         import torch.distributed as dist
         flat = torch.cat([p.detach().reshape(-1) for p in tr.net.parameters()])
         allw = [torch.empty_like(flat) for _ in range(ws)]
@@ -252,29 +266,27 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
     # device, so the replays are the same steps as the eager calls.
     graph = None
     if S == 1 and graphs:
-        try:
-            # the engine is joined before the capture and as its last call: a step
-            # leaves the next dispatch order on the engine's side stream, which a
-            # capture must not hold unjoined (hipErrorStreamCaptureUnjoined)
-            cap = torch.cuda.Stream(dev)
-            cap.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(cap):
-                engs[0].join()
-                for _ in range(2):
-                    best, _ = one_ply(engs[0], vh)
-                    engs[0].step(best, want_obs=False, want_info=False)
-                engs[0].join()
-            torch.cuda.synchronize(dev)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
-                for _ in range(2):
-                    best, _ = one_ply(engs[0], vh)
-                    engs[0].step(best, want_obs=False, want_info=False)
-                engs[0].join()
-            torch.cuda.synchronize(dev)
-        except Exception as ex:                        # eager launches then
-            print(f"[bench] C2 graph capture failed ({ex}); eager", file=sys.stderr)
-            graph = None
+        from bgx.graphs import capture
+        # the engine is joined before the capture and as its last call: a step
+        # leaves the next dispatch order on the engine's side stream, which a
+        # capture must not hold unjoined (hipErrorStreamCaptureUnjoined)
+        cap = torch.cuda.Stream(dev)
+        cap.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cap):
+            engs[0].join()
+            for _ in range(2):
+                best, _ = one_ply(engs[0], vh)
+                engs[0].step(best, want_obs=False, want_info=False)
+            engs[0].join()
+        torch.cuda.synchronize(dev)
+
+        def two_steps():
+            for _ in range(2):
+                best, _ = one_ply(engs[0], vh)
+                engs[0].step(best, want_obs=False, want_info=False)
+            engs[0].join()
+        graph = capture("c2", two_steps, cap)       # a failed capture ends the process
+        torch.cuda.synchronize(dev)
     barrier(ws)
     t0 = time.perf_counter()
     if graph is not None:
@@ -486,35 +498,30 @@ def main():
     G = args.graph_steps
     graphs = []                                         # graphs[g][k]: slots [gG, gG + G) of shard k
     if not args.no_graphs and args.workload == "c3" and G >= 2 and G % 2 == 0 and ring % G == 0:
-        try:
-            ctrs = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(S)]
-            caps = [torch.cuda.Stream(dev) for _ in range(S)]
+        from bgx.graphs import capture
+        ctrs = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in range(S)]
+        caps = [torch.cuda.Stream(dev) for _ in range(S)]
+        for k in range(S):
+            with torch.cuda.stream(streams[k]):
+                engs[k].join()
+        torch.cuda.synchronize(dev)
+
+        def graph_steps(k, g0):
+            e, b = engs[k], bufs[k]
+            for i in range(g0, g0 + G):
+                net.act(e, seed=4242 + rank * 16 + k, step=i, step_ctr=ctrs[k],
+                        out=(b["act"][i], b["logp"][i], b["value"][i]), records_out=b["records"][i])
+                e.step(b["act"][i], want_obs=False, want_info=False, out=(b["reward"][i], b["done"][i]))
+            e.join()
+            PolicyNet.advance_counter(ctrs[k], ring)
+        for g0 in range(0, ring, G):              # a failed capture ends the process (bgx/graphs.py)
+            graphs.append([capture("c3", lambda k=k, g0=g0: graph_steps(k, g0), caps[k]) for k in range(S)])
+        torch.cuda.synchronize(dev)
+        for row in graphs:                          # untimed: first replays upload the graphs
             for k in range(S):
                 with torch.cuda.stream(streams[k]):
-                    engs[k].join()
-            torch.cuda.synchronize(dev)
-            for g0 in range(0, ring, G):
-                row = []
-                for k in range(S):
-                    e, b, gr = engs[k], bufs[k], torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gr, stream=caps[k], capture_error_mode="thread_local"):
-                        for i in range(g0, g0 + G):
-                            net.act(e, seed=4242 + rank * 16 + k, step=i, step_ctr=ctrs[k],
-                                    out=(b["act"][i], b["logp"][i], b["value"][i]), records_out=b["records"][i])
-                            e.step(b["act"][i], want_obs=False, want_info=False, out=(b["reward"][i], b["done"][i]))
-                        e.join()
-                        PolicyNet.advance_counter(ctrs[k], ring)
-                    row.append(gr)
-                graphs.append(row)
-            torch.cuda.synchronize(dev)
-            for row in graphs:                          # untimed: first replays upload the graphs
-                for k in range(S):
-                    with torch.cuda.stream(streams[k]):
-                        row[k].replay()
-            torch.cuda.synchronize(dev)
-        except Exception as ex:
-            print(f"[bench] C3 graph capture failed ({ex}); eager", file=sys.stderr)
-            graphs = []
+                    row[k].replay()
+        torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
     barrier(ws)
     torch.cuda.synchronize(dev)
@@ -605,7 +612,7 @@ def main():
                      "mean_legal_moves": mean_moves},
     }
     line["per_rank"] = [{"rank": k, "env_steps": r[0], "seconds": r[1]} for k, r in enumerate(per_rank)]
-    if ws > 1:
+    if backend is not None:
         line["dist_backend"] = backend
     if args.mirror_steps > 0 and not args.host_mirror and args.workload == "c3":
         # north_star's "rollout into pinned host buffers": the same C3 step with every
@@ -658,7 +665,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if ws > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -145,6 +145,12 @@ int bgx_copy_lanes(bgx_engine* e, int32_t lane0, int32_t n, uint8_t* lanes_dst, 
  * re-enumerate their legal moves for the stored player/roll: lets a caller pose
  * arbitrary positions (tests, analysis).  lanes_src uint8[n][64] on the device. */
 int bgx_set_lanes(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_src, void* stream);
+/* bgx_set_lanes with regen = 0: the records are written as given and the stored
+ * legal moves / counts are left as they were -- the reference's BackgammonEnv.roll_dice
+ * and pass_turn change roll_result / current_player without touching legal_moves
+ * until update_legal_moves() runs (backgammon_env.py:198-251); regen = 1 is
+ * bgx_set_lanes (that update_legal_moves). */
+int bgx_set_lanes_ex(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_src, int32_t regen, void* stream);
 
 /* Sticky device error word (bit 0: a position overflowed the slow-path dedup
  * table).  Synchronises the engine's device. */

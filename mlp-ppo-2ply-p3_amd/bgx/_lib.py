@@ -37,6 +37,7 @@ SIGNATURES = {
     "bgx_action_masks": (ctypes.c_int, [_P, _P, _P, _P]),
     "bgx_copy_lanes": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P]),
     "bgx_set_lanes": (ctypes.c_int, [_P, _I32, _I32, _P, _P]),
+    "bgx_set_lanes_ex": (ctypes.c_int, [_P, _I32, _I32, _P, _I32, _P]),
     "bgx_engine_error": (ctypes.c_int, [_P, _P]),
     "bgx_policy_packed_size": (ctypes.c_int, [_I32, _I32]),
     "bgx_policy_pack": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P]),

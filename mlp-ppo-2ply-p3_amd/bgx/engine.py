@@ -167,9 +167,15 @@ class Engine:
               "bgx_copy_lanes")
         return out
 
-    def set_lanes(self, records: torch.Tensor, lane0: int = 0):
+    def set_lanes(self, records: torch.Tensor, lane0: int = 0, regen: bool = True):
+        """Overwrite lane records [lane0, lane0 + n); regen: re-enumerate their legal
+        moves for the stored player / roll (update_legal_moves), else leave the
+        stored moves as they are (roll_dice / pass_turn, bgx_set_lanes_ex)."""
         r = records.to(device=self.device, dtype=torch.uint8).contiguous()
-        check(self._lib.bgx_set_lanes(self._h, lane0, r.shape[0], _ptr(r), self._stream()), "bgx_set_lanes")
+        if r.dim() != 2 or r.shape[1] != 64:
+            raise ValueError(f"set_lanes: records must be [n, 64] bytes, got {tuple(r.shape)}")
+        check(self._lib.bgx_set_lanes_ex(self._h, lane0, r.shape[0], _ptr(r), int(bool(regen)), self._stream()),
+              "bgx_set_lanes_ex")
 
     def n_moves(self, out: torch.Tensor | None = None) -> torch.Tensor:
         """Legal-action count per lane (int16[B]); mask = arange(max_moves) < count."""

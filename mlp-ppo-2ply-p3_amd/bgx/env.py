@@ -173,8 +173,28 @@ class BackgammonEnv(_LaneView):
     def get_observation(self):
         return self.board.get_board_features(self.current_player).to(self.device)
 
-    def pass_turn(self):
-        raise NotImplementedError("turn passing happens inside step() on the device")
+    # The reference's step() calls these three in turn (backgammon_env.py:129-131,
+    # 186-188); here step() does the same on the device.  As public methods they
+    # edit the lane's record the way the reference edits its attributes:
+    # roll_dice and pass_turn leave legal_moves / action_mask stale until
+    # update_legal_moves() re-enumerates them.
+    def _write_record(self, rec: np.ndarray, regen: bool):
+        self._eng.set_lanes(torch.from_numpy(np.ascontiguousarray(rec, dtype=np.uint8))[None], 0, regen=regen)
+        self._invalidate()
+
+    def update_legal_moves(self):                   # :198-243
+        self._write_record(self._record(), regen=True)
+
+    def roll_dice(self):                            # :245-246, numpy's global stream
+        rec = self._record().copy()
+        rec[53] = np.random.randint(1, 7)
+        rec[54] = np.random.randint(1, 7)
+        self._write_record(rec, regen=False)
+
+    def pass_turn(self):                            # :248-251
+        rec = self._record().copy()
+        rec[52] ^= 1
+        self._write_record(rec, regen=False)
 
     def check_for_gammon(self, player: Player) -> bool:        # :365-373
         return int(self.board.tensor[3, 1 - int(player)]) == 0

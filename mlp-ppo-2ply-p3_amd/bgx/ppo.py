@@ -48,10 +48,12 @@ def _world(group) -> int:
 
 
 def allreduce_mean_(tensors, group=None):
-    """Average a list of tensors across ranks in ONE flat bucket (one collective)."""
-    ws = _world(group)
-    if ws == 1 or not tensors:
+    """Average a list of tensors across ranks in ONE flat bucket (one collective).
+    Runs whenever a process group is initialised, also at world size 1 (the
+    one-rank RCCL test exercises the collective that way)."""
+    if not (dist.is_available() and dist.is_initialized()) or not tensors:
         return
+    ws = _world(group)
     flat = torch.cat([t.reshape(-1).float() for t in tensors])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     flat /= ws

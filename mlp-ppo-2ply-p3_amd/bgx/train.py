@@ -52,6 +52,7 @@ import ctypes
 from . import _lib
 from ._lib import check
 from .engine import Engine, encode_records
+from .graphs import capture
 from .policy import PolicyNet, MASK_LOG
 from .ppo import (EPS_CLIP, GAMMA, LEARNING_RATE, NUM_EPOCHS, VALUE_LOSS_COEF, ENTROPY_COEF_START,
                   ENTROPY_COEF_END, ENTROPY_ANNEAL_EPISODES, allreduce_mean_, global_normalize, _world)
@@ -554,7 +555,8 @@ class PPOTrainer:
         """One graph per (slot pair, shard): act + step for slots t and t + 1 with the
         noise step read from the shard's device counter (advanced by 2 per replay),
         the engine joined at the end (its side-stream dispatch order).  Thread-local
-        capture mode: a communicator's watchdog thread may query events meanwhile."""
+        capture mode: a communicator's watchdog thread may query events meanwhile.
+        A failed capture is terminal (bgx/graphs.py)."""
         self._ctrs = [torch.zeros(1, dtype=torch.int32, device=self.dev) for _ in range(self.S)]
         caps = [torch.cuda.Stream(self.dev) for _ in range(self.S)]
         for k in range(self.S):
@@ -562,18 +564,15 @@ class PPOTrainer:
             with torch.cuda.stream(caps[k]):
                 self.engs[k].join()
         torch.cuda.synchronize(self.dev)
-        graphs = []
-        for t in range(0, self.T, 2):
-            row = []
-            for k in range(self.S):
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=caps[k], capture_error_mode="thread_local"):
-                    for j in range(2):
-                        self._act_step(k, t + j, j, self._ctrs[k])
-                    self.engs[k].join()
-                    PolicyNet.advance_counter(self._ctrs[k], 2)
-                row.append(g)
-            graphs.append(row)
+        def two_steps(k, t):
+            for j in range(2):
+                self._act_step(k, t + j, j, self._ctrs[k])
+            self.engs[k].join()
+            PolicyNet.advance_counter(self._ctrs[k], 2)
+        # a failed capture ends the process (bgx/graphs.py: the engines' host state has
+        # advanced through steps that never ran)
+        graphs = [[capture("trainer", lambda k=k, t=t: two_steps(k, t), caps[k]) for k in range(self.S)]
+                  for t in range(0, self.T, 2)]
         torch.cuda.synchronize(self.dev)
         self._graphs = graphs
 
@@ -607,12 +606,7 @@ class PPOTrainer:
         for st in self._streams[1:]:
             cur.wait_stream(st)
         if self.graphs and self._graphs is None:
-            try:
-                self._capture()
-            except RuntimeError as ex:           # eager rollouts then (same results)
-                torch.cuda.synchronize(self.dev)
-                print(f"[bgx] rollout graph capture failed ({ex}); eager rollouts", flush=True)
-                self.graphs, self._graphs = False, None
+            self._capture()
         st = episode_stats(buf["rewards"], buf["dones"], buf["records"][:, :, 52], self.ep_carry)
         if _world(self.group) > 1:
             dist.all_reduce(st, group=self.group)

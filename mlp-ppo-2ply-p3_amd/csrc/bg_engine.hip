@@ -937,12 +937,17 @@ int bgx_copy_lanes(bgx_engine* e, int32_t lane0, int32_t n, uint8_t* lanes_dst, 
 }
 
 int bgx_set_lanes(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_src, void* stream) {
+    return bgx_set_lanes_ex(e, lane0, n, lanes_src, 1, stream);
+}
+
+int bgx_set_lanes_ex(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_src, int32_t regen, void* stream) {
     if (!e || !lanes_src || lane0 < 0 || n < 0 || lane0 + n > e->a.B) return BGX_EINVAL;
     if (n == 0) return BGX_OK;
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
     CK(hipMemcpyAsync(A.lanes + (size_t)lane0 * 64, lanes_src, (size_t)n * 64, hipMemcpyDeviceToDevice, s));
+    if (!regen) return BGX_OK;
     CK(hipMemsetAsync(A.ovf_count, 0, 16, s));
     LAUNCH_LOG(e, k_regen, dim3(n), s, A, lane0);
     CKL();

@@ -32,6 +32,42 @@ def test_backgammon_env_trace(bgx, golden):
             assert np.array_equal(bgx.types.tensor_to52(env.board.tensor).numpy(), g["board_after"][j])
 
 
+def test_env_public_turn_methods_trace(bgx, golden):
+    """pass_turn / roll_dice / update_legal_moves (backgammon_env.py:198-251) as
+    public methods: at every G4 row where the mover has no legal move the
+    reference's step() runs exactly pass_turn(); roll_dice(); update_legal_moves()
+    (:124-131), so the test calls the three instead of step() there and the rest
+    of the reference game must follow unchanged.  Also checks the intermediate
+    states: roll_dice alone leaves the legal moves stale (as the reference's
+    attributes stay until update_legal_moves)."""
+    g = golden("traces")
+    games = sorted({int(x) for x in g["game"][g["kind"] == 1]})[:12]
+    manual = 0
+    for gi in games:
+        sel = np.where(g["game"] == gi)[0]
+        env = bgx.BackgammonEnv(match_length=15 if gi % 5 else 3)
+        env.seed(gi)
+        env.reset()
+        for j in sel:
+            assert env.roll_result == [int(g["r0"][j]), int(g["r1"][j])]
+            assert int(env.action_mask.sum()) == g["n_legal"][j]
+            assert int(env.current_player) == g["mover"][j]
+            if g["kind"][j] == 1:                                # "No legal actions, turn passed"
+                before = int(env.current_player)
+                env.pass_turn()
+                assert int(env.current_player) == 1 - before and int(env.action_mask.sum()) == 0
+                env.roll_dice()
+                assert int(env.action_mask.sum()) == 0             # stale until update_legal_moves
+                env.update_legal_moves()
+                manual += 1
+                assert int(env.current_player) == g["player_after"][j]
+            else:
+                _, rew, done, _ = env.step(int(g["action"][j]))
+                assert float(rew) == g["reward"][j] and done == bool(g["done"][j])
+            assert np.array_equal(bgx.types.tensor_to52(env.board.tensor).numpy(), g["board_after"][j])
+    assert manual >= 20
+
+
 def test_vectorized_env_trace(bgx, golden):
     g = golden("traces")
     n_env = g["vec_obs0"].shape[0]
