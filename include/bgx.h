@@ -308,6 +308,19 @@ int bgx_ppo_gw2(const void* h_dev, const int32_t* perm_dev, const void* stats_de
                 int32_t hidden, int32_t n_actions, const void* w2h_dev, const void* b2h_dev, float k1,
                 const int32_t* plan_dev, float* workspace_dev, float* gw2_dev, float* gb2_dev, void* stream);
 
+/* The fp16 epoch's fc1 weight and bias gradients straight from the records
+ * (replaces, inside ppo_agent.py:268-305 under autocast, the weight-gradient GEMM
+ * dh^T x of policy_network.py:69-70 over materialised fp16 feature rows):
+ * gw1 [128][208] fp32 += dh^T [x | 1 | 0], x = the 198 fp16 features of each
+ * 64-byte record (off / 15 rounded as autocast rounds it), column 198 = gb1,
+ * 199..207 += 0.  dh [m][128] fp16 (bgx_ppo_rows' output) and records [m][64] in
+ * the same row order, both 16-byte aligned; hidden = 128; workspace of
+ * bgx_ppo_gw1_workspace(m) bytes (16-byte aligned).  Deterministic (fixed-order
+ * partial sums). */
+int64_t bgx_ppo_gw1_workspace(int32_t m);
+int bgx_ppo_gw1(const void* dh_dev, const uint8_t* records_dev, int32_t m, int32_t hidden, float* workspace_dev,
+                float* gw1_dev, void* stream);
+
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
  * evaluation after it (k_eval, the MFMA kernel). */

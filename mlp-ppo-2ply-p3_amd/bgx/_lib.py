@@ -67,6 +67,8 @@ SIGNATURES = {
                                     ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _I32, _P]),
     "bgx_ppo_gw2_workspace": (ctypes.c_int64, [_I32]),
     "bgx_ppo_gw2": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P]),
+    "bgx_ppo_gw1_workspace": (ctypes.c_int64, [_I32]),
+    "bgx_ppo_gw1": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),
 }

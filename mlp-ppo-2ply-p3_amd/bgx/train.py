@@ -373,9 +373,10 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
     (bgx_ppo_rows + bgx_ppo_gw2): fc1 from the records (bgx_fc1_records), then per
     row the logits, the loss head, dy and dh = ReLU'(h) fp16(dy W2h) on MFMA without
     the [n, 512] logits in HBM; gW2 / gb2 = dy^T [h | 1] from per-row statistics;
-    gW1 / gb1 = dh^T [x | 1] (the ones column of the 208-wide feature rows).  Same
-    fp16 operands, fp32 accumulation and per-row gradient scaling as
-    _ppo_epoch_amp_manual; gradients land in p.grad as fp32."""
+    gW1 / gb1 = dh^T [x | 1] with x generated from the records on chip (bgx_ppo_gw1:
+    no feature rows in HBM).  Same fp16 operands, fp32 accumulation and per-row
+    gradient scaling as _ppo_epoch_amp_manual; gradients land in p.grad as fp32.
+    The chunks' feature entries are not read."""
     eps, c_v, c_e, gscale = coefs
     row_scale = gscale * n_total / min(n_total, REF_ROWS)
     post = min(n_total, REF_ROWS) / n_total
@@ -400,16 +401,10 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         w1pack = torch.empty(L.bgx_fc1_packed_size(Hd), dtype=torch.uint8, device=dev)
         check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
-        for feats, _legal, actions, old_logp, returns, adv, records, *extra in chunks:
+        for _feats, _legal, actions, old_logp, returns, adv, records, *extra in chunks:
             prep = extra[0] if extra else {}
             rec = records.contiguous()
             m = rec.shape[0]
-            if prep.get("bias_col"):                # 208-wide fp16 rows with ones in column 198
-                x = feats
-            else:
-                x = torch.zeros(m, 208, dtype=torch.float16, device=dev)
-                x[:, :F_in] = feats[:, :F_in]
-                x[:, FEAT_BIAS_COL] = 1.0
             perm, plan, row_plan = prep["plan"] if "plan" in prep else ppo_row_plan(rec, A)
             h = torch.empty(m, Hd, dtype=torch.float16, device=dev)
             check(L.bgx_fc1_records(p(rec), m, p(w1pack), p(b1h), Hd, p(h), stream), "bgx_fc1_records")
@@ -426,7 +421,9 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
             ws = torch.empty(L.bgx_ppo_gw2_workspace(m) // 4, dtype=torch.float32, device=dev)
             check(L.bgx_ppo_gw2(p(h), pp, p(stats), p(info), m, Hd, A, p(W2h), p(b2h), k1, p(plan), p(ws),
                                 p(gW2), p(gb2), stream), "bgx_ppo_gw2")
-            gW1 += _wgrad(dh, x)
+            # dh is in the order of rec (bgx_ppo_rows writes it in the original row order)
+            ws1 = torch.empty(L.bgx_ppo_gw1_workspace(m) // 4, dtype=torch.float32, device=dev)
+            check(L.bgx_ppo_gw1(p(dh), p(rec), m, Hd, p(ws1), p(gW1), stream), "bgx_ppo_gw1")
         if post != 1.0:
             for t in (gW1, gW2, gb2):
                 t.mul_(post)
@@ -644,24 +641,25 @@ class PPOTrainer:
         # (fp16 under autocast: 2^21 rows x 198 x 2 B = 0.8 GB of HBM)
         manual = self.fused and self.amp and os.environ.get("BGX_PPO_MANUAL", "1") != "0" and _is_policy_mlp(self.net)
         fused_head = manual and _fused_head_ok(self.net)
-        feats = [encode_records(recs[s:min(N, s + self.chunk)], torch.float16 if self.amp else torch.float32,
-                                width=208 if fused_head else (FEAT_W if manual else 198))
+        # the fused head generates every feature it needs from the records (fc1 forward,
+        # gW1); the other paths read features encoded once for the 4 epochs
+        feats = [None if fused_head else
+                 encode_records(recs[s:min(N, s + self.chunk)], torch.float16 if self.amp else torch.float32,
+                                width=FEAT_W if manual else 198)
                  for s in range(0, N, self.chunk)] if self.fused else None
         preps = [{} for _ in range(0, N, self.chunk)]
         sorted_rows = [None for _ in range(0, N, self.chunk)]
         if fused_head:
             # once per update: each chunk's rows in the order of the fused head's row plan
             # (by the number of action tiles a row needs), gathered so that every kernel
-            # of the 4 epochs reads them contiguously; the ones column (fc1's bias gradient)
+            # of the 4 epochs reads them contiguously
             for i, s in enumerate(range(0, N, self.chunk)):
                 e = min(N, s + self.chunk)
                 perm, plan, row_plan = ppo_row_plan(recs[s:e], self.A)
                 pl = perm.long()
                 sorted_rows[i] = (recs[s:e][pl].contiguous(), acts[s:e][pl].contiguous(), old[s:e][pl].contiguous(),
                                   R[s:e][pl].contiguous(), adv[s:e][pl].contiguous())
-                feats[i] = encode_records(sorted_rows[i][0], torch.float16, width=208)
-                feats[i][:, FEAT_BIAS_COL] = 1.0
-                preps[i] = {"bias_col": True, "plan": (None, plan, row_plan)}
+                preps[i] = {"plan": (None, plan, row_plan)}
 
         def chunks():
             for i, s in enumerate(range(0, N, self.chunk)):

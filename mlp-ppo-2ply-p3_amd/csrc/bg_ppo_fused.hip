@@ -609,6 +609,136 @@ __global__ __launch_bounds__(256) void k_ppo_gw2_sum2(const float* __restrict__ 
     else gb2[32 * at + (e - 32 * kH)] += s;
 }
 
+
+// ---- gW1 / gb1 of the fp16 epoch straight from the records (fc1 of
+// policy_network.py:69-70 under autocast; ppo_agent.py:268-305's backward):
+// gw1[u][f] = sum over rows of dh[row][u] * x[row][f], x = [the 198 features (fp16,
+// as autocast casts them) | 1 (column 198: gb1) | 0], fp32 accumulation.  The
+// round-3 epoch read 208-wide fp16 feature rows materialised once per update
+// (0.8 GB) through a split-K hipBLASLt GEMM; here the features are generated on
+// chip from the 64-byte records.  The reduction axis is the row, so both MFMA
+// operands need 8 consecutive rows per lane: dh [32 rows][128] is staged in a
+// swizzled LDS image and read transposed (tr_operand), the records are staged
+// TRANSPOSED ([byte][row]) so that one 32-bit LDS read yields a byte for 4
+// consecutive rows.  A workgroup = 7 waves, wave fb owning features 32fb..32fb+31
+// (224 >= 199) as the A operand (lane = feature) and all 4 unit blocks as B: 4
+// accumulators, 8 MFMAs per 32-row tile.  Every feature is one byte value v (a
+// point count, bar, off, or the mover) through clamp(v * a + b, 0, c):
+// n >= k: (1, -(k - 1), 1); (n - 3) / 2 for n >= 3: (1/2, -3/2, 64); bar / 2:
+// (1/2, 0, 64); off / 15: (1/15, 0, 1) (fp16(v * fp32(1/15)) == fp16(fp32(v / 15))
+// for v = 0..15); mover one-hot: (-1, 1, 1) / (1, 0, 1); ones column (0, 1, 1).
+constexpr int kFB = 7;                      // feature blocks of 32
+constexpr int kW1 = 208;                    // gw1 row width (198 features, ones column, zeros)
+constexpr int kGw1Part = kFB * 32 * kH;     // floats per workgroup partial, [224][128]
+constexpr int kGw1Grid = 512;               // workgroups (2 per CU)
+
+__device__ __forceinline__ void gw1_param(int f, int& byte, float& fa, float& fbias, float& fc) {
+    byte = 0; fa = 0.0f; fbias = 0.0f; fc = 0.0f;
+    if (f < 196) {
+        const int p = f >= 98 ? 1 : 0, q = f - 98 * p;
+        if (q < 96) {
+            const int k = q & 3;
+            byte = 24 * p + (q >> 2);
+            if (k < 3) { fa = 1.0f; fbias = -(float)k; fc = 1.0f; }
+            else { fa = 0.5f; fbias = -1.5f; fc = 64.0f; }
+        } else if (q == 96) { byte = 48 + p; fa = 0.5f; fc = 64.0f; }
+        else { byte = 50 + p; fa = 1.0f / 15.0f; fc = 1.0f; }
+    } else if (f < 198) { byte = 52; fa = f == 196 ? -1.0f : 1.0f; fbias = f == 196 ? 1.0f : 0.0f; fc = 1.0f; }
+    else if (f == 198) { fbias = 1.0f; fc = 1.0f; }
+}
+
+struct Gw1Args {
+    const _Float16* dh;         // [m][128]
+    const uint8_t* rec;         // [m][64], the same row order
+    int m, tiles_per_wg;
+    float* part;                // [grid][224][128]
+};
+
+__global__ __launch_bounds__(448) void k_ppo_gw1(Gw1Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t sdh[2][32 * 256];
+    __shared__ __attribute__((aligned(16))) uint8_t srt[2][56 * 32];
+    const int tid = threadIdx.x, fb = tid >> 6, hh = (tid >> 5) & 1;
+    const int ntiles = (a.m + 31) >> 5;
+    const int t0 = blockIdx.x * a.tiles_per_wg, t1 = min(t0 + a.tiles_per_wg, ntiles);
+    int byte;
+    float fa, fbias, fc;
+    gw1_param(32 * fb + (tid & 31), byte, fa, fbias, fc);
+    f32x16 acc[4];
+    #pragma unroll
+    for (int u = 0; u < 4; ++u)
+        #pragma unroll
+        for (int i = 0; i < 16; ++i) acc[u][i] = 0.0f;
+    // loaders: dh = 512 16-byte chunks per tile (threads take chunk tid, and tid + 448
+    // for tid < 64); records = 32 rows x 14 dwords (bytes 0..55), one per thread
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    uint4 d0 = z4, d1 = z4;
+    uint32_t rw = 0;
+    const int rr = tid / 14, rwd = tid - 14 * (tid / 14);
+    auto load = [&](int tile) {
+        const int row0 = tile * 32;
+        d0 = row0 + (tid >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (tid >> 4)) * kH))[tid & 15] : z4;
+        if (tid < 64) {
+            const int i = tid + 448;
+            d1 = row0 + (i >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (i >> 4)) * kH))[i & 15] : z4;
+        }
+        const int gr = row0 + rr < a.m ? row0 + rr : a.m - 1;
+        rw = ((const uint32_t*)(a.rec + (size_t)gr * 64))[rwd];
+    };
+    if (t0 < t1) load(t0);
+    int buf = 0;
+    for (int tile = t0; tile < t1; ++tile, buf ^= 1) {
+        *(uint4*)(sdh[buf] + swz(tid >> 4, tid & 15)) = d0;
+        if (tid < 64) *(uint4*)(sdh[buf] + swz((tid + 448) >> 4, (tid + 448) & 15)) = d1;
+        #pragma unroll
+        for (int q = 0; q < 4; ++q) srt[buf][(4 * rwd + q) * 32 + rr] = (uint8_t)(rw >> (8 * q));
+        __syncthreads();
+        if (tile + 1 < t1) load(tile + 1);                 // next tile in flight behind the MFMAs
+        #pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const uint8_t* bp = srt[buf] + byte * 32 + 16 * s + 4 * hh;
+            const uint32_t w0 = *(const uint32_t*)bp, w1 = *(const uint32_t*)(bp + 8);
+            f16x8 A;
+            #pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                A[j] = (_Float16)fminf(fmaxf(fmaf((float)((w0 >> (8 * j)) & 255u), fa, fbias), 0.0f), fc);
+                A[4 + j] = (_Float16)fminf(fmaxf(fmaf((float)((w1 >> (8 * j)) & 255u), fa, fbias), 0.0f), fc);
+            }
+            #pragma unroll
+            for (int u = 0; u < 4; ++u)
+                acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, tr_operand(sdh[buf], 0, s, u, laundered_lane()),
+                                                                acc[u], 0, 0, 0);
+        }
+    }
+    // C = [32 features][32 units] per u: lane = unit 32u + (l & 31), register i = feature (i&3) + 8(i>>2) + 4hh
+    float* out = a.part + (size_t)blockIdx.x * kGw1Part;
+    #pragma unroll
+    for (int u = 0; u < 4; ++u)
+        #pragma unroll
+        for (int i = 0; i < 16; ++i)
+            out[(32 * fb + (i & 3) + 8 * (i >> 2) + 4 * hh) * kH + 32 * u + (tid & 31)] = acc[u][i];
+}
+
+// gw1[u][f] += the workgroups' partials [f][u], summed in a fixed order (group g sums
+// workgroups g, g + kRed, ...; then the kRed group sums), f < 208
+__global__ __launch_bounds__(256) void k_ppo_gw1_sum1(const float* __restrict__ part, int nwg, float* __restrict__ part2) {
+    const int g = blockIdx.y;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kGw1Part) return;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    int w = g, k = 0;
+    for (; w < nwg; w += kRed, k = (k + 1) & 3) acc[k] += part[(size_t)w * kGw1Part + e];
+    part2[(size_t)g * kGw1Part + e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+__global__ __launch_bounds__(256) void k_ppo_gw1_sum2(const float* __restrict__ part2, float* __restrict__ gw1) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kW1 * kH) return;
+    float s = 0.0f;
+    #pragma unroll 8
+    for (int g = 0; g < kRed; ++g) s += part2[(size_t)g * kGw1Part + e];
+    const int f = e / kH, u = e - kH * f;
+    gw1[u * kW1 + f] += s;
+}
+
 }  // namespace
 
 extern int bgx_internal_fail(hipError_t e);
@@ -667,6 +797,33 @@ extern "C" int bgx_ppo_gw2(const void* h, const int32_t* perm, const void* stats
     float* part2 = workspace + (size_t)max_tasks * kPart;
     hipLaunchKernelGGL(k_ppo_gw2_sum1, dim3((kPart + 255) / 256, kNT, kRed), dim3(256), 0, s, workspace, plan, part2);
     hipLaunchKernelGGL(k_ppo_gw2_sum2, dim3((kPart + 255) / 256, kNT), dim3(256), 0, s, part2, gw2, gb2);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
+
+extern "C" int64_t bgx_ppo_gw1_workspace(int32_t m) {
+    if (m < 0) return BGX_EINVAL;
+    const int64_t ntiles = (m + 31) / 32;
+    const int64_t wgs = ntiles < kGw1Grid ? (ntiles > 0 ? ntiles : 1) : kGw1Grid;
+    return (wgs + kRed) * kGw1Part * (int64_t)sizeof(float);
+}
+
+extern "C" int bgx_ppo_gw1(const void* dh, const uint8_t* records, int32_t m, int32_t hidden, float* workspace,
+                           float* gw1, void* stream) {
+    if (hidden != kH || m < 0) return BGX_EINVAL;
+    if (m == 0) return BGX_OK;
+    if (!dh || !records || !workspace || !gw1) return BGX_EINVAL;
+    if (((uintptr_t)dh | (uintptr_t)records) % 16 || (uintptr_t)workspace % 16) return BGX_EINVAL;
+    const int ntiles = (m + 31) / 32;
+    const int wgs = ntiles < kGw1Grid ? ntiles : kGw1Grid;
+    const int per = (ntiles + wgs - 1) / wgs;
+    Gw1Args a{(const _Float16*)dh, records, m, per, workspace};
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_ppo_gw1, dim3(wgs), dim3(448), 0, s, a);
+    float* part2 = workspace + (size_t)wgs * kGw1Part;
+    hipLaunchKernelGGL(k_ppo_gw1_sum1, dim3((kGw1Part + 255) / 256, kRed), dim3(256), 0, s, workspace, wgs, part2);
+    hipLaunchKernelGGL(k_ppo_gw1_sum2, dim3((kW1 * kH + 255) / 256), dim3(256), 0, s, part2, gw1);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }

@@ -42,6 +42,8 @@ def lib():
         L.bgo_features.argtypes = [P, ctypes.c_int, P]
         L.bgo_features_batch.argtypes = [P, P, ctypes.c_int, P]
         L.bgo_movegen_batch.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, P, P]
+        L.bgo_two_ply_leaves.argtypes = [P, ctypes.c_int, ctypes.c_uint64, P, ctypes.c_int, P]
+        L.bgo_two_ply_leaves.restype = ctypes.c_int
         L.bgo_mt_seed.argtypes = [P, ctypes.c_uint32]
         L.bgo_mt_next.argtypes = [P]
         L.bgo_mt_next.restype = ctypes.c_uint32
@@ -103,6 +105,19 @@ def features_batch(boards52, players):
     out = np.zeros((b.shape[0], 198), dtype=np.float32)
     lib().bgo_features_batch(_p(b), _p(p), b.shape[0], _p(out))
     return out
+
+
+def two_ply_leaves(board52, mover: int, move: int, cap: int = 1 << 16):
+    """Leaf features [rows, 198] of one root move over the 21 rolls and the leaf
+    count per roll (bgo_two_ply_leaves)."""
+    b = np.ascontiguousarray(board52, dtype=np.int8)
+    while True:
+        out = np.empty((cap, 198), dtype=np.float32)
+        counts = np.zeros(21, dtype=np.int32)
+        n = lib().bgo_two_ply_leaves(_p(b), int(mover), ctypes.c_uint64(int(move)), _p(out), cap, _p(counts))
+        if n >= 0:
+            return out[:n], counts
+        cap *= 4
 
 
 class MT:

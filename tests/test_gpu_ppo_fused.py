@@ -146,3 +146,40 @@ def test_fused_head_row_order_invariant():
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
         assert _rel(b[2], a[2]) < 1e-6 and _rel(b[3], a[3]) < 1e-6
         assert torch.allclose(a[4] / m, b[4] / m, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("m", [33, 4096 * 8 - 5, 1 << 18])
+def test_gw1_from_records_matches_feature_gemm(m):
+    """bgx_ppo_gw1 (gW1 / gb1 = dh^T [x | 1] with x generated on chip from the
+    records) against the GEMM it replaces over the encoded fp16 feature rows
+    (encode_records, pinned to the reference's features by G2), in fp64: the
+    same fp16 operands, so only the fp32 accumulation order differs.  Ragged m
+    (partial last row tile), records from a real rollout (every feature type:
+    bar, off, one-hot, the ones column)."""
+    from bgx import _lib
+    from bgx._lib import check
+    from bgx.engine import encode_records
+    L = _lib.load()
+    recs = _setup(seed=5, batch=4096, horizon=8)[0]
+    reps = (m + recs.shape[0] - 1) // recs.shape[0]
+    recs = recs.repeat(reps, 1)[:m].contiguous()
+    g = torch.Generator(device="cuda").manual_seed(m)
+    dh = (torch.randn(m, 128, device="cuda", generator=g) * 0.5).half()
+    dh[torch.rand(m, 128, device="cuda", generator=g) < 0.4] = 0          # the ReLU mask's zeros
+    gw1 = torch.zeros(128, 208, dtype=torch.float32, device="cuda")
+    ws = torch.empty(L.bgx_ppo_gw1_workspace(m) // 4, dtype=torch.float32, device="cuda")
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for _ in range(2):                                                   # accumulates (+=)
+        check(L.bgx_ppo_gw1(_p(dh), _p(recs), m, 128, _p(ws), _p(gw1), s), "bgx_ppo_gw1")
+    x = encode_records(recs, torch.float16, width=208)
+    x[:, 198] = 1.0
+    ref = 2 * (dh.double().t() @ x.double())
+    assert torch.equal(gw1[:, 199:], torch.zeros_like(gw1[:, 199:]))
+    err = (gw1.double() - ref).abs()
+    assert float(err.max()) <= 1e-5 * float(ref.abs().max()) + 1e-6, float(err.max())
+    assert _rel(gw1.double(), ref) < 1e-6
+    # deterministic: the same call gives the same bits
+    gw1b = torch.zeros_like(gw1)
+    for _ in range(2):
+        check(L.bgx_ppo_gw1(_p(dh), _p(recs), m, 128, _p(ws), _p(gw1b), s), "bgx_ppo_gw1")
+    assert torch.equal(gw1, gw1b)

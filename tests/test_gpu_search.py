@@ -98,6 +98,75 @@ def test_two_ply_vs_oracle_composition(setup):
     assert stats["afterstates"] == int(n_all.sum()) and stats["jobs"] == 21 * int(n_all.sum())
 
 
+@pytest.fixture(scope="module")
+def targeted_roots():
+    """>= 100 root positions picked from a seeded random-policy population
+    (2,048 MT lanes, several game ages): 40 plain, 20 with the mover on the bar
+    (bar entries), 20 in the bear-off (mover has borne off), 20 with a doubles
+    roll.  Returns their 64-byte records."""
+    import bgx
+    eng = bgx.Engine(batch=2048, max_moves=500, dice="mt", auto_reset=True)
+    eng.seed(np.arange(7000, 7000 + 2048, dtype=np.uint32))
+    eng.reset()
+    rng = np.random.RandomState(11)
+    want = {"plain": 40, "bar": 20, "bearoff": 20, "doubles": 20}
+    got = {k: [] for k in want}
+    for t in range(1, 241):
+        nm = eng.n_moves().cpu().numpy()
+        eng.step(torch.from_numpy(np.array([rng.randint(k) if k else 0 for k in nm], np.int32)).cuda())
+        if t % 20:
+            continue
+        rec = eng.records().cpu().numpy()
+        for i in rng.permutation(len(rec))[:256]:
+            r = rec[i]
+            n, m = int(r[60]) | (int(r[61]) << 8), int(r[52])
+            if n == 0 or n > 120 or r[55]:               # bounded oracle time per root
+                continue
+            cls = ("bar" if r[48 + m] > 0 else "bearoff" if r[50 + m] > 0 else
+                   "doubles" if r[53] == r[54] else "plain")
+            if len(got[cls]) < want[cls] and (cls != "plain" or t % 60 == 0):
+                got[cls].append(r.copy())
+        if all(len(got[k]) == want[k] for k in want):
+            break
+    assert all(len(got[k]) == want[k] for k in want), {k: len(v) for k, v in got.items()}
+    return np.stack([r for k in want for r in got[k]])
+
+
+def test_two_ply_targeted_roots_vs_oracle(setup, targeted_roots):
+    """Q of every move of 100 targeted roots (bar entries, bear-offs, doubles,
+    plain; replies with bar entries and doubles reply sets over 100 moves occur
+    among their jobs) against the oracle composition bgo_two_ply_leaves + the
+    torch fp32 value head: within 1e-5, same first argmax, exact leaf counts."""
+    bgx, net, vh, _ = setup
+    from bgx.search import two_ply
+    R = targeted_roots
+    eng = bgx.Engine(batch=len(R), max_moves=500, dice="mt", auto_reset=True)
+    eng.set_lanes(torch.from_numpy(R))
+    best, bestq, q, stats = two_ply(eng, vh, want_q=True)
+    rec, mv, _ = eng.lanes()
+    rec, mv = rec.cpu().numpy(), mv.cpu().numpy().view(np.uint64)
+    q, best = q.cpu().numpy(), best.cpu().numpy()
+    assert np.array_equal(rec[:, :60], R[:, :60])
+    leaves = big = 0
+    for i in range(len(R)):
+        n = int(rec[i, 60]) | (int(rec[i, 61]) << 8)
+        board, mover = rec[i, :52].view(np.int8), int(rec[i, 52])
+        ref_moves, _ = O.movegen(board, mover, (int(rec[i, 53]), int(rec[i, 54])))
+        assert np.array_equal(mv[i, :n], ref_moves[:500]), i
+        Q = np.zeros(n, np.float32)
+        for a in range(n):
+            feats, counts = O.two_ply_leaves(board, mover, int(mv[i, a]))
+            v = _V(net, feats)
+            seg = np.minimum.reduceat(v, np.concatenate([[0], np.cumsum(counts)[:-1]]))
+            Q[a] = float(np.dot(PROBS.astype(np.float64), seg.astype(np.float64)))
+            leaves += int(counts.sum())
+            big += int((counts[[0, 6, 11, 15, 18, 20]] > 100).sum())
+        assert np.abs(q[i, :n] - Q).max() < TOL, i
+        assert abs(Q[best[i]] - Q.max()) < TOL, i
+    assert stats["leaves"] == leaves
+    assert big >= 20, big                              # doubles reply sets over 100 moves
+
+
 def test_two_ply_pool_retry_rounds(setup, monkeypatch):
     """A leaf pool far too small for one pass: lost jobs are re-run in later
     rounds; Q, the choice and the exact leaf count must not change."""
