@@ -421,8 +421,8 @@ def main():
         "done": torch.empty(ring, Bs, dtype=torch.uint8, **kw),
     } for _ in range(S)]
     want_mirror = args.host_mirror or args.mirror_steps > 0
-    pins = [{k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in b.items()}
-            for b in bufs] if want_mirror else None
+    from bgx.hostcopy import HostMirror
+    mirrors = [HostMirror(b) for b in bufs] if want_mirror else None     # pinned twins of the rings
     copy_streams = [torch.cuda.Stream(dev) for _ in range(S)] if want_mirror else None
     counts = [torch.empty(Bs, dtype=torch.int16, device=dev) for _ in range(S)]
     gen = torch.Generator(device=dev).manual_seed(99 + rank)
@@ -458,9 +458,7 @@ def main():
             if state["mirror"]:                                   # pinned-host mirror (side stream)
                 cs = copy_streams[k]
                 cs.wait_stream(st)
-                with torch.cuda.stream(cs):
-                    for name in b:
-                        pins[k][name][slot].copy_(b[name][slot], non_blocking=True)
+                mirrors[k].copy(slot, 1, stream=cs)                # every field of the slot, one launch
                 if slot == ring - 1:
                     st.wait_stream(cs)                            # the ring wraps: rows must be on the host
 
@@ -616,14 +614,64 @@ def main():
         line["dist_backend"] = backend
     if args.mirror_steps > 0 and not args.host_mirror and args.workload == "c3":
         # north_star's "rollout into pinned host buffers": the same C3 step with every
-        # rollout row also copied to pinned host memory on a side stream (PCIe-inclusive)
-        state["mirror"] = True
+        # rollout row also copied to pinned host memory.  Graph form (default): each
+        # shard's 2-step graph also carries, on a forked copy stream, ONE bgx_copy_regions
+        # launch for the previous slot pair of every field (bgx.hostcopy), so the copy of
+        # pair p overlaps the steps of pair p + 1; eager form (--no-graphs, and a short
+        # comparison run): one copy launch per step and shard after the step.
+        mirror = {"config": "C3 as the headline + every rollout row (64-B record, action, log-prob, value, reward, "
+                            "done: 81 B per lane-step) copied to pinned host memory",
+                  "host_bytes_per_step_per_gpu": B * 81}
+        torch.cuda.synchronize(dev)
+        if graphs:
+            from bgx.graphs import capture
+            mgraphs = []
+
+            def mirror_steps(k, g0):
+                e, b, cs = engs[k], bufs[k], copy_streams[k]
+                cs.wait_stream(torch.cuda.current_stream(dev))
+                mirrors[k].copy((g0 - G) % ring, G, stream=cs)      # the previous pair, beside these steps
+                graph_steps(k, g0)
+                torch.cuda.current_stream(dev).wait_stream(cs)
+            for g0 in range(0, ring, G):
+                mgraphs.append([capture("c3-mirror", lambda k=k, g0=g0: mirror_steps(k, g0), caps[k])
+                                for k in range(S)])
+            torch.cuda.synchronize(dev)
+            for row in mgraphs:                     # untimed upload replays
+                for k in range(S):
+                    with torch.cuda.stream(streams[k]):
+                        row[k].replay()
+            torch.cuda.synchronize(dev)
+            nrep = max(1, args.mirror_steps // G)
+            barrier(ws)
+            t0 = time.perf_counter()
+            for r in range(nrep):
+                row = mgraphs[r % len(mgraphs)]
+                for k in range(S):
+                    with torch.cuda.stream(streams[k]):
+                        row[k].replay()
+            last = ((nrep - 1) % len(mgraphs)) * G          # the last replayed pair: its own copy
+            for k in range(S):
+                with torch.cuda.stream(streams[k]):
+                    copy_streams[k].wait_stream(streams[k])
+                    mirrors[k].copy(last, G, stream=copy_streams[k])
+                    streams[k].wait_stream(copy_streams[k])
+            torch.cuda.synchronize(dev)
+            barrier(ws)
+            elm = max_over_ranks(time.perf_counter() - t0, ws)
+            msteps = nrep * G
+            mirror.update({"env_steps_per_s": sum_over_ranks(float(B * msteps), ws) / elm,
+                           "ms_per_step": elm * 1e3 / msteps, "steps": msteps,
+                           "form": f"HIP graphs of {G} steps per shard, each with one copy launch (6 fields) "
+                                   "of the previous slot pair on a forked stream"})
+        state["mirror"] = True                       # eager form: one copy launch per step and shard
+        esteps = args.mirror_steps if not graphs else min(args.mirror_steps, 16)
         for _ in range(2):
             step(False)
         torch.cuda.synchronize(dev)
         barrier(ws)
         t0 = time.perf_counter()
-        for _ in range(args.mirror_steps):
+        for _ in range(esteps):
             step(False)
         for cs in copy_streams:
             torch.cuda.current_stream(dev).wait_stream(cs)
@@ -631,12 +679,14 @@ def main():
         barrier(ws)
         elm = max_over_ranks(time.perf_counter() - t0, ws)
         state["mirror"] = False
-        line["host_mirror"] = {
-            "config": "C3 as the headline + every rollout row (64-B record, action, log-prob, value, reward, "
-                      "done: 81 B per lane-step) copied to pinned host memory on a side stream per shard",
-            "env_steps_per_s": sum_over_ranks(float(B * args.mirror_steps), ws) / elm,
-            "ms_per_step": elm * 1e3 / args.mirror_steps, "steps": args.mirror_steps,
-            "host_bytes_per_step_per_gpu": B * 81}
+        eager = {"env_steps_per_s": sum_over_ranks(float(B * esteps), ws) / elm, "ms_per_step": elm * 1e3 / esteps,
+                 "steps": esteps}
+        if graphs:
+            mirror["eager"] = eager
+        else:
+            mirror.update(eager)
+            mirror["form"] = "eager launches, one copy launch (6 fields) per step and shard"
+        line["host_mirror"] = mirror
     if sq and sq.get("instructions_per_lane_step") and args.workload == "c3":
         line["roofline_issue"] = issue_roofline(sq, Bs, kern_ms, summ.get("pmc_command"))
     if args.two_ply_batches > 0:

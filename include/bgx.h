@@ -152,6 +152,23 @@ int bgx_set_lanes(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_
  * bgx_set_lanes (that update_legal_moves). */
 int bgx_set_lanes_ex(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lanes_src, int32_t regen, void* stream);
 
+/* Rollout rows to pinned host memory (the reference keeps its rollout memory on
+ * the host, ppo_agent.py:175-187): up to BGX_MAX_COPY_REGIONS strided 2-D copies in
+ * ONE kernel launch, so a HIP graph of rollout steps can carry the copy of a slot
+ * pair of every field as one node.  Region i copies `rows` rows of `width` bytes
+ * from src (row pitch spitch) to dst (pitch dpitch); device pointers on both sides
+ * (a pinned host buffer's device pointer from bgx_host_device_ptr); widths,
+ * pitches and pointers 16-byte aligned.  workgroups <= 0: up to 64. */
+#define BGX_MAX_COPY_REGIONS 8
+typedef struct {
+    const void* src;
+    void* dst;
+    int64_t width, rows, spitch, dpitch;
+} bgx_region;
+int bgx_copy_regions(const bgx_region* regions, int32_t n, int32_t workgroups, void* stream);
+/* The device-side address of pinned (hipHostMalloc / torch pin_memory) host memory. */
+int bgx_host_device_ptr(void* host_ptr, void** dev_ptr_out);
+
 /* Sticky device error word (bit 0: a position overflowed the slow-path dedup
  * table).  Synchronises the engine's device. */
 int bgx_engine_error(bgx_engine* e, int32_t* err_out);

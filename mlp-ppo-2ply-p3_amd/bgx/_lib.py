@@ -69,6 +69,8 @@ SIGNATURES = {
     "bgx_ppo_gw2": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P]),
     "bgx_ppo_gw1_workspace": (ctypes.c_int64, [_I32]),
     "bgx_ppo_gw1": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P]),
+    "bgx_copy_regions": (ctypes.c_int, [_P, _I32, _I32, _P]),
+    "bgx_host_device_ptr": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),
 }
@@ -100,6 +102,14 @@ def embedded_build_id(path: str = LIB_PATH):
     data = open(path, "rb").read()
     i = data.find(BUILD_ID_TAG)
     return data[i + len(BUILD_ID_TAG):i + len(BUILD_ID_TAG) + 64].decode() if i >= 0 else None
+
+
+class BgxRegion(ctypes.Structure):
+    _fields_ = [("src", _P), ("dst", _P), ("width", ctypes.c_int64), ("rows", ctypes.c_int64),
+                ("spitch", ctypes.c_int64), ("dpitch", ctypes.c_int64)]
+
+
+MAX_COPY_REGIONS = 8           # include/bgx.h BGX_MAX_COPY_REGIONS
 
 
 class BgxBuffers(ctypes.Structure):

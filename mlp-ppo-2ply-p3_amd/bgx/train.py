@@ -53,6 +53,7 @@ from . import _lib
 from ._lib import check
 from .engine import Engine, encode_records
 from .graphs import capture
+from .hostcopy import HostMirror
 from .policy import PolicyNet, MASK_LOG
 from .ppo import (EPS_CLIP, GAMMA, LEARNING_RATE, NUM_EPOCHS, VALUE_LOSS_COEF, ENTROPY_COEF_START,
                   ENTROPY_COEF_END, ENTROPY_ANNEAL_EPISODES, allreduce_mean_, global_normalize, _world)
@@ -497,8 +498,9 @@ class PPOTrainer:
         # rollout steps replayed as HIP graphs (2 steps per graph, one graph per slot pair
         # and shard), captured at the end of the first rollout: the engines' host state is
         # then a 2-step fixed point (bench.py C3).  Equal to the eager rollout
-        # (tests/test_gpu_train.py::test_rollout_graphs_match_eager).
-        self.graphs = (self.dev.type == "cuda" and horizon % 2 == 0 and not pinned) if graphs is None else graphs
+        # (tests/test_gpu_train.py::test_rollout_graphs_match_eager).  With pinned=True each
+        # graph also carries the host copy of the previous slot pair (bgx.hostcopy).
+        self.graphs = (self.dev.type == "cuda" and horizon % 2 == 0) if graphs is None else graphs
         self._graphs = None
         torch.manual_seed(seed)
         self.net = PolicyNet(hidden_size=hidden, action_size=n_actions).to(self.dev)
@@ -524,15 +526,28 @@ class PPOTrainer:
                     "rewards": torch.empty(T, B, dtype=torch.float32, **kw),
                     "dones": torch.empty(T, B, dtype=torch.uint8, **kw)}
         self.pinned = None
-        if pinned:
-            self.pinned = {k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in self.buf.items()}
-            self.copy_stream = torch.cuda.Stream(self.dev)
+        if pinned:                      # the rollout mirrored into pinned host memory
+            self.mirror = HostMirror(self.buf)
+            self.pinned = self.mirror.host
         self.ep_carry = torch.zeros(B, dtype=torch.float64, **kw)     # train.py:58 episode_rewards
         self.last_episode_stats = None
         for e in self.engs:
             e.reset(want_obs=False)
         self._streams = ([torch.cuda.current_stream(self.dev)] + [torch.cuda.Stream(self.dev) for _ in range(self.S - 1)]
                          if self.dev.type == "cuda" else [None])
+        # per shard: the stream its host copies run on (beside the next steps)
+        self._copy_streams = [torch.cuda.Stream(self.dev) for _ in range(self.S)] if pinned else None
+
+    def _mirror_slots(self, k: int, t0: int, n: int):
+        """Shard k's rows of slots [t0, t0 + n) to the pinned host buffers, on the shard's
+        copy stream forked from its step stream (joined later by _join_copies)."""
+        cs = self._copy_streams[k]
+        cs.wait_stream(torch.cuda.current_stream(self.dev))
+        lo = k * (self.B // self.S)
+        self.mirror.copy(t0, n, lo, lo + self.B // self.S, stream=cs)
+
+    def _join_copies(self, k: int):
+        torch.cuda.current_stream(self.dev).wait_stream(self._copy_streams[k])
 
     def _slot(self, k: int, t: int):
         """Shard k's views of rollout slot t (contiguous row ranges)."""
@@ -562,10 +577,14 @@ class PPOTrainer:
                 self.engs[k].join()
         torch.cuda.synchronize(self.dev)
         def two_steps(k, t):
+            if self.pinned is not None and t >= 2:      # the previous pair's rows, beside these steps
+                self._mirror_slots(k, t - 2, 2)
             for j in range(2):
                 self._act_step(k, t + j, j, self._ctrs[k])
             self.engs[k].join()
             PolicyNet.advance_counter(self._ctrs[k], 2)
+            if self.pinned is not None and t >= 2:
+                self._join_copies(k)
         # a failed capture ends the process (bgx/graphs.py: the engines' host state has
         # advanced through steps that never ran)
         graphs = [[capture("trainer", lambda k=k, t=t: two_steps(k, t), caps[k]) for k in range(self.S)]
@@ -589,17 +608,22 @@ class PPOTrainer:
                     with torch.cuda.stream(self._streams[k]):
                         row[k].replay()
             self.step_counter += self.T
+            if self.pinned is not None:          # the last pair (each graph copies the pair before it)
+                for k in range(self.S):
+                    with torch.cuda.stream(self._streams[k]):
+                        self._mirror_slots(k, self.T - 2, 2)
+                        self._join_copies(k)
         for t in range(self.T if self._graphs is None else 0):
             for k in range(self.S):
                 with torch.cuda.stream(self._streams[k]):
                     self._act_step(k, t, self.step_counter)
+                    if self.pinned is not None:
+                        self._mirror_slots(k, t, 1)
             self.step_counter += 1
-            if self.pinned is not None:
-                for st in self._streams:
-                    self.copy_stream.wait_stream(st)
-                with torch.cuda.stream(self.copy_stream):
-                    for k in buf:
-                        self.pinned[k][t].copy_(buf[k][t], non_blocking=True)
+        if self.pinned is not None and self._graphs is None:
+            for k in range(self.S):
+                with torch.cuda.stream(self._streams[k]):
+                    self._join_copies(k)
         for st in self._streams[1:]:
             cur.wait_stream(st)
         if self.graphs and self._graphs is None:

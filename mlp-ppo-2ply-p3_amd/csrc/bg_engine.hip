@@ -25,6 +25,8 @@
 using namespace bg;
 
 namespace {
+
+constexpr int kMaxRegions = BGX_MAX_COPY_REGIONS;
 using namespace bg;
 
 // -------------------------------------------------------------- kernels --
@@ -458,6 +460,31 @@ __global__ void k_mt_seed(uint32_t* mt, const uint32_t* seeds, int B) {
     s[0] = x;
     for (int i = 1; i < 624; ++i) { x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i; s[i] = x; }
     s[624] = 624u;
+}
+
+
+// ---- rollout rows to pinned host memory (bgx_copy_regions): up to 8 strided 2-D
+// copies in one launch, 16 bytes per thread-step, non-temporal stores (the
+// destination is host memory across PCIe; nothing on the device reads it back).
+struct CopyRegions {
+    const uint8_t* src[kMaxRegions];
+    uint8_t* dst[kMaxRegions];
+    int64_t wchunks[kMaxRegions], spitch[kMaxRegions], dpitch[kMaxRegions];
+    int64_t pre[kMaxRegions + 1];               // chunk prefix over the regions
+    int n;
+};
+
+__global__ __launch_bounds__(256) void k_copy_regions(CopyRegions R) {
+    const int64_t total = R.pre[R.n];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        int r = 0;
+        #pragma unroll
+        for (int k = 1; k < kMaxRegions; ++k) r += (k < R.n && i >= R.pre[k]) ? 1 : 0;
+        const int64_t j = i - R.pre[r], row = j / R.wchunks[r], col = j - row * R.wchunks[r];
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = *(const u32x4*)(R.src[r] + row * R.spitch[r] + 16 * col);
+        __builtin_nontemporal_store(v, (u32x4*)(R.dst[r] + row * R.dpitch[r] + 16 * col));
+    }
 }
 
 thread_local std::string g_err;
@@ -959,6 +986,38 @@ int bgx_engine_error(bgx_engine* e, int32_t* err_out) {
     CK(hipSetDevice(e->device));
     CK(hipDeviceSynchronize());
     CK(hipMemcpy(err_out, e->a.err, 4, hipMemcpyDeviceToHost));
+    return BGX_OK;
+}
+
+int bgx_host_device_ptr(void* host_ptr, void** dev_ptr_out) {
+    if (!host_ptr || !dev_ptr_out) return BGX_EINVAL;
+    CK(hipHostGetDevicePointer(dev_ptr_out, host_ptr, 0));
+    return BGX_OK;
+}
+
+int bgx_copy_regions(const bgx_region* regions, int32_t n, int32_t workgroups, void* stream) {
+    if (!regions || n < 0 || n > kMaxRegions) return BGX_EINVAL;
+    CopyRegions R;
+    memset(&R, 0, sizeof R);
+    R.n = n;
+    int64_t acc = 0;
+    for (int i = 0; i < n; ++i) {
+        const bgx_region& g = regions[i];
+        if (!g.src || !g.dst || g.width < 0 || g.rows < 0 || g.width % 16 || g.spitch % 16 || g.dpitch % 16 ||
+            (uintptr_t)g.src % 16 || (uintptr_t)g.dst % 16 || (g.rows > 1 && (g.spitch < g.width || g.dpitch < g.width)))
+            return BGX_EINVAL;
+        R.src[i] = (const uint8_t*)g.src; R.dst[i] = (uint8_t*)g.dst;
+        R.wchunks[i] = g.width / 16 > 0 ? g.width / 16 : 1;
+        R.spitch[i] = g.spitch; R.dpitch[i] = g.dpitch;
+        R.pre[i] = acc;
+        acc += g.width / 16 * g.rows;
+    }
+    for (int i = n; i <= kMaxRegions; ++i) R.pre[i] = acc;
+    if (acc == 0) return BGX_OK;
+    const int64_t need = (acc + 255) / 256;
+    const int wg = (int)(workgroups > 0 && workgroups < need ? workgroups : (need < 64 ? need : 64));
+    hipLaunchKernelGGL(k_copy_regions, dim3(wg), dim3(256), 0, (hipStream_t)stream, R);
+    CKL();
     return BGX_OK;
 }
 

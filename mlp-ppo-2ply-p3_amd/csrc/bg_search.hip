@@ -907,6 +907,152 @@ void k_eval(EvalArgs E) {
     }
 }
 
+// ---- round 4: the evaluator with W1 resident in registers ----
+// k_eval above reads every W1 fragment from LDS just before the MFMA that uses it
+// (2 waves/SIMD at H = 128: no registers to prefetch a k-block ahead), so most MFMAs
+// wait on an LDS read (60 % MFMA busy).  Here no weight is loaded in the K loop:
+//  * wide (H > 64): a workgroup of NW = slices/2 waves, wave T holding unit tile T's
+//    hi and lo fragments for all 13 k-blocks (104 VGPRs) and its 32 head weights.
+//    The waves take the SAME 64 leaves (2 x 32 columns) per iteration, each
+//    generating their features in registers (7 VALU per k-block and leaf tile,
+//    hidden in the gaps of its 2 MFMAs) -- so no LDS traffic in the K loop at all --
+//    and each forms its 32 units' part of V; the parts meet in LDS (fixed order
+//    T = 0..NW-1, then + bias) and waves 0 and 1 finish one leaf tile each
+//    (segmented min, atomicMin per job).  One barrier per iteration (the part
+//    array is double-buffered).
+//  * narrow (H <= 48): one wave holds every tile's fragments (13 x NT uint4; 156
+//    VGPRs at H = 40) and walks its own 32-leaf tiles; the head weights (epilogue
+//    only) stay in LDS.
+template <int NT>
+__global__ __launch_bounds__(64 * (slices(NT) / 2)) __attribute__((amdgpu_waves_per_eu(2)))
+void k_eval_rw_wide(EvalArgs E) {
+    static_assert(wide_tiles(NT), "wide form");
+    constexpr int NW = slices(NT) / 2, NS = slices(NT);
+    __shared__ float part[2][NW][64];
+    const int l = lane_id(), h = l >> 5, c = l & 31, wv = threadIdx.x >> 6;
+    uint4 wh[kKB], wl[kKB];
+    #pragma unroll
+    for (int kb = 0; kb < kKB; ++kb) {
+        wh[kb] = E.w1q[((kb * NS + 2 * wv + 0) * 64) + l];
+        wl[kb] = E.w1q[((kb * NS + 2 * wv + 1) * 64) + l];
+    }
+    float4 hw[4];
+    #pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) hw[r4] = reinterpret_cast<const float4*>(E.wvq)[(wv * 4 + r4) * 64 + l];
+    const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
+    const unsigned long long tiles = used / 64;
+    unsigned long long tile = *E.lo / 64 + blockIdx.x;
+    if (tile >= tiles) return;                      // the whole workgroup: same tiles for every wave
+    LeafRaw raw[2];
+    LeafRow row[2];
+    #pragma unroll
+    for (int n = 0; n < 2; ++n) { raw[n] = load_raw(E, tile * 64 + 32 * n + c); row[n] = load_row(E, raw[n]); }
+    int buf = 0;
+    for (; tile < tiles; tile += gridDim.x, buf ^= 1) {
+        Leaf L[2];
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) L[n] = make_leaf(raw[n], row[n]);
+        const unsigned long long nxt = tile + gridDim.x < tiles ? tile + gridDim.x : tile;
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
+        f32x16 x0, x1;
+        #pragma unroll
+        for (int kb = 0; kb < kKB; ++kb) {
+            const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
+            const f16x8 ah = __builtin_bit_cast(f16x8, wh[kb]), al = __builtin_bit_cast(f16x8, wl[kb]);
+            x0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, kb == 0 ? (f32x16){} : x0, 0, 0, 0);
+            x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f1, kb == 0 ? (f32x16){} : x1, 0, 0, 0);
+            x0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f0, x0, 0, 0, 0);
+            x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f1, x1, 0, 0, 0);
+        }
+        #pragma unroll
+        for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
+        float a0 = 0.0f, a1 = 0.0f;
+        #pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+            a0 = fmaf(relu_raw(x0[4 * r4 + 0]), hw[r4].x, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 0]), hw[r4].x, a1);
+            a0 = fmaf(relu_raw(x0[4 * r4 + 1]), hw[r4].y, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 1]), hw[r4].y, a1);
+            a0 = fmaf(relu_raw(x0[4 * r4 + 2]), hw[r4].z, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 2]), hw[r4].z, a1);
+            a0 = fmaf(relu_raw(x0[4 * r4 + 3]), hw[r4].w, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 3]), hw[r4].w, a1);
+        }
+        a0 += __shfl_xor(a0, 32);
+        a1 += __shfl_xor(a1, 32);
+        if (h == 0) { part[buf][wv][c] = a0; part[buf][wv][32 + c] = a1; }
+        __syncthreads();
+        if (wv < 2) {                                // wave n finishes leaf tile n
+            float vv = part[buf][0][32 * wv + c];
+            #pragma unroll
+            for (int t = 1; t < NW; ++t) vv += part[buf][t][32 * wv + c];
+            vv += E.bv;
+            const int jb = wv == 0 ? L[0].job : L[1].job;
+            if (!(wv == 0 ? L[0].valid : L[1].valid)) vv = INFINITY;
+            #pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const float v2 = __shfl_down(vv, o, 32);
+                const int j2 = __shfl_down(jb, o, 32);
+                if (c + o < 32 && j2 == jb) vv = fminf(vv, v2);
+            }
+            const int jp = __shfl_up(jb, 1, 32);
+            if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
+        }
+    }
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_eval_rw_narrow(EvalArgs E) {
+    static_assert(NT <= 3, "narrow register form: at most 3 tiles (156 VGPRs of weights)");
+    __shared__ float wvs[NT * 8 * 64];
+    for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = E.wvq[i];
+    __syncthreads();
+    const int l = lane_id(), h = l >> 5, c = l & 31;
+    uint4 wq[NT][kKB];
+    #pragma unroll
+    for (int t = 0; t < NT; ++t)
+        #pragma unroll
+        for (int kb = 0; kb < kKB; ++kb) wq[t][kb] = E.w1q[(kb * NT + t) * 64 + l];
+    const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
+    const unsigned long long tiles = used / 32;
+    const unsigned long long stride = (unsigned long long)gridDim.x * 4;
+    unsigned long long tile = *E.lo / 32 + (unsigned long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= tiles) return;
+    LeafRaw raw = load_raw(E, tile * 32 + c);
+    LeafRow row = load_row(E, raw);
+    for (; tile < tiles; tile += stride) {
+        const Leaf L = make_leaf(raw, row);
+        const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
+        raw = load_raw(E, nxt * 32 + c);
+        f32x16 x[NT];
+        #pragma unroll
+        for (int kb = 0; kb < kKB; ++kb) {
+            const f16x8 f = feat16(L, kb, h);
+            #pragma unroll
+            for (int t = 0; t < NT; ++t)
+                x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wq[t][kb]), f,
+                                                              kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+        }
+        row = load_row(E, raw);
+        float v = 0.0f;
+        #pragma unroll
+        for (int t = 0; t < NT; ++t)
+            #pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int r = j < 4 ? j : j + 4;
+                v = fmaf(fmaxf(x[t][r] + x[t][r + 4], 0.0f), wvs[(t * 8 + j) * 64 + l], v);
+            }
+        v += __shfl_xor(v, 32) + E.bv;
+        const int jb = L.job;
+        float vv = L.valid ? v : INFINITY;
+        #pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const float v2 = __shfl_down(vv, o, 32);
+            const int j2 = __shfl_down(jb, o, 32);
+            if (c + o < 32 && j2 == jb) vv = fminf(vv, v2);
+        }
+        const int jp = __shfl_up(jb, 1, 32);
+        if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
+    }
+}
+
 // 1-ply: V of every row's afterstate (the row's "no reply" leaf: rowkey + rowside),
 // 64 rows per tile, grid-stride over ceil(*nrows / 64) tiles.
 struct EvalRowsArgs {
@@ -1110,10 +1256,19 @@ static int persistent_grid(const bgx_engine* e, K kernel, int per_cu_cap) {
 
 typedef void (*EvalFn)(EvalArgs);
 typedef void (*EvalRowsFn)(EvalRowsArgs);
-static EvalFn eval_kernel(int NT) {
+// the 2-ply evaluator for NT 16-unit slices and its workgroup size: W1 in registers
+// (k_eval_rw_*) except at NT = 4 (208 VGPRs of weights in one wave; LDS weights)
+struct EvalPick { EvalFn fn; int threads; };
+static EvalPick eval_kernel(int NT) {
     switch (NT) {
-        case 1: return k_eval<1>; case 2: return k_eval<2>; case 3: return k_eval<3>; case 4: return k_eval<4>;
-        case 5: return k_eval<5>; case 6: return k_eval<6>; case 7: return k_eval<7>; default: return k_eval<8>;
+        case 1: return {k_eval_rw_narrow<1>, 256};
+        case 2: return {k_eval_rw_narrow<2>, 256};
+        case 3: return {k_eval_rw_narrow<3>, 256};
+        case 4: return {k_eval<4>, 64 * BGX_EVAL_NARROW_WAVES};
+        case 5: return {k_eval_rw_wide<5>, 64 * (slices(5) / 2)};
+        case 6: return {k_eval_rw_wide<6>, 64 * (slices(6) / 2)};
+        case 7: return {k_eval_rw_wide<7>, 64 * (slices(7) / 2)};
+        default: return {k_eval_rw_wide<8>, 64 * (slices(8) / 2)};
     }
 }
 static EvalRowsFn eval_rows_kernel(int NT) {
@@ -1345,8 +1500,12 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         E.keys = S.keys;
         E.tags = S.tags;
         S.cap = E.cap = (unsigned long long)pcap;
-        const EvalFn keval = eval_kernel(NT);
-        const int g_eval = eval_grid(e, keval, NT);
+        const EvalPick keval = eval_kernel(NT);
+        int occ_eval = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_eval, keval.fn, keval.threads, 0) != hipSuccess ||
+            occ_eval <= 0)
+            occ_eval = 1;
+        const int g_eval = occ_eval * persistent_grid(e, keval.fn, 1);     // resident workgroups
         if (!e->search_ev[0])
             for (hipEvent_t& ev : e->search_ev) SCK(hipEventCreate(&ev));
         const char* ov = getenv("BGX_2PLY_OVERLAP");    // "0": enumerators back to back (A/B)
@@ -1362,7 +1521,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         }
         SCK(hipEventRecord(e->search_ev[0], s));
         auto eval = [&](hipStream_t st) {
-            hipLaunchKernelGGL(keval, dim3(g_eval), dim3(64 * eval_waves(NT)), 0, st, E);
+            hipLaunchKernelGGL(keval.fn, dim3(g_eval), dim3(keval.threads), 0, st, E);
         };
         // retry rounds run few waves: every wave holding a block wastes its unused
         // part, and a round must leave pool for its jobs to finish (progress with any pool)

@@ -38,6 +38,12 @@ def test_trainer_iteration():
     assert bool((r[~d] == 0).all()) and bool(torch.isin(r[d], torch.tensor([1.0, 1.5, 2.0], device="cuda")).all())
     m2 = tr.iteration()
     assert np.isfinite(m2["total_loss"])
+    # the second rollout was replayed from HIP graphs, each carrying the pinned-host copy
+    # of the previous slot pair (bgx.hostcopy): every field of every slot on the host
+    assert tr._graphs is not None
+    torch.cuda.synchronize()
+    for k, v in tr.buf.items():
+        assert torch.equal(tr.pinned[k], v.cpu()), k
     # episode metrics (train.py:64-99): every finished self-play episode is a win for
     # its last mover, and its reward is that win's reward (no other rewards occur)
     for _ in range(16):
