@@ -624,46 +624,38 @@ def main():
                   "host_bytes_per_step_per_gpu": B * 81}
         torch.cuda.synchronize(dev)
         if graphs:
-            from bgx.graphs import capture
-            mgraphs = []
-
-            def mirror_steps(k, g0):
-                e, b, cs = engs[k], bufs[k], copy_streams[k]
-                cs.wait_stream(torch.cuda.current_stream(dev))
-                mirrors[k].copy((g0 - G) % ring, G, stream=cs)      # the previous pair, beside these steps
-                graph_steps(k, g0)
-                torch.cuda.current_stream(dev).wait_stream(cs)
-            for g0 in range(0, ring, G):
-                mgraphs.append([capture("c3-mirror", lambda k=k, g0=g0: mirror_steps(k, g0), caps[k])
-                                for k in range(S)])
-            torch.cuda.synchronize(dev)
-            for row in mgraphs:                     # untimed upload replays
-                for k in range(S):
-                    with torch.cuda.stream(streams[k]):
-                        row[k].replay()
-            torch.cuda.synchronize(dev)
+            # the headline's graphs, each shard's replayed pair followed by ONE copy launch of
+            # that pair's rows (bgx_copy_regions, all 6 fields) on the shard's copy stream; the
+            # copy of pair p runs beside the steps of pair p + 1.  The copy streams are joined
+            # only when the ring wraps (before a pair's slots are overwritten).  (Round 4 first
+            # captured the copy inside each graph as a forked branch: the graph's join then held
+            # every pair to its copy, 179 M vs 248 M env steps/s for the eager form.)
             nrep = max(1, args.mirror_steps // G)
+            for k in range(S):                      # the eager timing steps left side-stream work
+                with torch.cuda.stream(streams[k]):
+                    engs[k].join()
+            torch.cuda.synchronize(dev)
             barrier(ws)
             t0 = time.perf_counter()
             for r in range(nrep):
-                row = mgraphs[r % len(mgraphs)]
+                g = r % len(graphs)
                 for k in range(S):
                     with torch.cuda.stream(streams[k]):
-                        row[k].replay()
-            last = ((nrep - 1) % len(mgraphs)) * G          # the last replayed pair: its own copy
+                        if g == 0 and r > 0:
+                            streams[k].wait_stream(copy_streams[k])     # the ring wraps
+                        graphs[g][k].replay()
+                        copy_streams[k].wait_stream(streams[k])
+                        mirrors[k].copy(g * G, G, stream=copy_streams[k])
             for k in range(S):
-                with torch.cuda.stream(streams[k]):
-                    copy_streams[k].wait_stream(streams[k])
-                    mirrors[k].copy(last, G, stream=copy_streams[k])
-                    streams[k].wait_stream(copy_streams[k])
+                streams[k].wait_stream(copy_streams[k])
             torch.cuda.synchronize(dev)
             barrier(ws)
             elm = max_over_ranks(time.perf_counter() - t0, ws)
             msteps = nrep * G
             mirror.update({"env_steps_per_s": sum_over_ranks(float(B * msteps), ws) / elm,
                            "ms_per_step": elm * 1e3 / msteps, "steps": msteps,
-                           "form": f"HIP graphs of {G} steps per shard, each with one copy launch (6 fields) "
-                                   "of the previous slot pair on a forked stream"})
+                           "form": f"the headline's HIP graphs ({G} steps per shard), each replayed pair followed by "
+                                   "one copy launch (6 fields) on the shard's copy stream"})
         state["mirror"] = True                       # eager form: one copy launch per step and shard
         esteps = args.mirror_steps if not graphs else min(args.mirror_steps, 16)
         for _ in range(2):

@@ -243,14 +243,10 @@ def _wgrad(g: torch.Tensor, x: torch.Tensor, splits: int = 64) -> torch.Tensor:
 REF_ROWS = 4096
 
 # Feature row width of the manual fp16 epoch: 208 = 198 features + 10 zero columns,
-# so fc1's forward GEMM and weight gradient read 16-byte aligned rows (396-byte rows
-# keep hipBLASLt off its vector-load kernels; tools/gemm_probe_pad.py).  The zero
-# columns meet zero weight columns: every product is unchanged.  BGX_PPO_FEAT_W=198 A/B.
-FEAT_W = int(os.environ.get("BGX_PPO_FEAT_W", "208"))
-# fc1's forward in the manual fp16 epoch runs from the stored records
-# (bgx_fc1_records: 64 B per row instead of the 416-byte feature row + hipBLASLt
-# GEMM); BGX_PPO_FC1=blas keeps the GEMM for A/B.
-FC1_FROM_RECORDS = os.environ.get("BGX_PPO_FC1", "records") != "blas"
+# so fc1's weight-gradient GEMM reads 16-byte aligned rows (396-byte rows keep
+# hipBLASLt off its vector-load kernels; tools/gemm_probe_pad.py).  The zero columns
+# meet zero weight columns: every product is unchanged.
+FEAT_W = 208
 
 
 def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
@@ -284,7 +280,7 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
         p = lambda t: ctypes.c_void_p(t.data_ptr())
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         colsum = torch.empty(PPO_COLSUM_BLOCKS, 512, dtype=torch.float32, device=dev)
-        fc1_rec = FC1_FROM_RECORDS and L.bgx_fc1_packed_size(Hd) > 0
+        fc1_rec = L.bgx_fc1_packed_size(Hd) > 0        # else the GEMM over the feature rows
         if fc1_rec:                                 # W1h in the record kernel's fragment order
             w1pack = torch.empty(L.bgx_fc1_packed_size(Hd), dtype=torch.uint8, device=dev)
             check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
@@ -329,10 +325,6 @@ def _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums):
 
 
 PPO_GW2_TASK_TILES = 32        # include/bgx.h BGX_PPO_GW2_TASK_TILES
-# The fp16 epoch's output layer + loss head as two HIP kernels without materialised
-# logits (csrc/bg_ppo_fused.hip); BGX_PPO_FUSED=0 keeps the round-2 manual epoch
-# (hipBLASLt head GEMM + bgx_ppo_head_ex + dy W2h + ReLU backward + split-K gW2) for A/B.
-PPO_FUSED_HEAD = os.environ.get("BGX_PPO_FUSED", "1") != "0"
 FEAT_BIAS_COL = 198            # the ones column of the 208-wide rows: gW1[:, 198] = gb1
 
 
@@ -366,7 +358,10 @@ def ppo_row_plan(records: torch.Tensor, n_actions: int = 500):
 
 
 def _fused_head_ok(net) -> bool:
-    return PPO_FUSED_HEAD and net.fc1.out_features == 128 and net.action_head.out_features == 500
+    """The fused output layer + loss head (csrc/bg_ppo_fused.hip) is built for the
+    reference's shape (H = 128, 500 actions); other shapes take the manual epoch
+    (hipBLASLt head GEMM + bgx_ppo_head_ex + dy W2h + ReLU backward + split-K gW2)."""
+    return net.fc1.out_features == 128 and net.action_head.out_features == 500
 
 
 def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
@@ -442,7 +437,7 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
         scale = 1.0
     sums = torch.zeros(3, dtype=torch.float64, device=dev)
     coefs = (EPS_CLIP, VALUE_LOSS_COEF, float(entropy_coef), float(scale) / n_total)
-    manual = amp and os.environ.get("BGX_PPO_MANUAL", "1") != "0" and _is_policy_mlp(net)
+    manual = amp and _is_policy_mlp(net)
     if manual:
         if _fused_head_ok(net):
             _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums)
@@ -499,7 +494,8 @@ class PPOTrainer:
         # and shard), captured at the end of the first rollout: the engines' host state is
         # then a 2-step fixed point (bench.py C3).  Equal to the eager rollout
         # (tests/test_gpu_train.py::test_rollout_graphs_match_eager).  With pinned=True each
-        # graph also carries the host copy of the previous slot pair (bgx.hostcopy).
+        # replayed pair's rows go to the host by one copy launch (bgx.hostcopy) on the
+        # shard's copy stream, beside the next pair's steps.
         self.graphs = (self.dev.type == "cuda" and horizon % 2 == 0) if graphs is None else graphs
         self._graphs = None
         torch.manual_seed(seed)
@@ -509,8 +505,8 @@ class PPOTrainer:
                 dist.broadcast(p.data, src=0, group=process_group)
         # ppo_agent.py:83 Adam; on the GPU the fused kernel: GradScaler hands it the scale and
         # the inf flag as device tensors, so an optimizer step needs no host sync
-        # (the foreach path's found_inf.item() left ~115 us idle per epoch).  BGX_ADAM_FUSED=0 A/B.
-        fused_adam = self.dev.type == "cuda" and os.environ.get("BGX_ADAM_FUSED", "1") != "0"
+        # (the foreach path's found_inf.item() left ~115 us idle per epoch)
+        fused_adam = self.dev.type == "cuda"
         self.opt = torch.optim.Adam(self.net.parameters(), lr=LEARNING_RATE, fused=fused_adam)
         self.scaler = GradScaler(device=self.dev.type)
         self.total_episodes = 0
@@ -577,14 +573,10 @@ class PPOTrainer:
                 self.engs[k].join()
         torch.cuda.synchronize(self.dev)
         def two_steps(k, t):
-            if self.pinned is not None and t >= 2:      # the previous pair's rows, beside these steps
-                self._mirror_slots(k, t - 2, 2)
             for j in range(2):
                 self._act_step(k, t + j, j, self._ctrs[k])
             self.engs[k].join()
             PolicyNet.advance_counter(self._ctrs[k], 2)
-            if self.pinned is not None and t >= 2:
-                self._join_copies(k)
         # a failed capture ends the process (bgx/graphs.py: the engines' host state has
         # advanced through steps that never ran)
         graphs = [[capture("trainer", lambda k=k, t=t: two_steps(k, t), caps[k]) for k in range(self.S)]
@@ -603,15 +595,16 @@ class PPOTrainer:
             for k in range(self.S):
                 with torch.cuda.stream(self._streams[k]):
                     self._ctrs[k].fill_(self.step_counter)
-            for row in self._graphs:             # the shards' replays side by side
+            for t, row in zip(range(0, self.T, 2), self._graphs):     # the shards' replays side by side
                 for k in range(self.S):
                     with torch.cuda.stream(self._streams[k]):
                         row[k].replay()
+                        if self.pinned is not None:  # the pair's rows to the host beside the next pair
+                            self._mirror_slots(k, t, 2)
             self.step_counter += self.T
-            if self.pinned is not None:          # the last pair (each graph copies the pair before it)
+            if self.pinned is not None:
                 for k in range(self.S):
                     with torch.cuda.stream(self._streams[k]):
-                        self._mirror_slots(k, self.T - 2, 2)
                         self._join_copies(k)
         for t in range(self.T if self._graphs is None else 0):
             for k in range(self.S):
@@ -663,7 +656,7 @@ class PPOTrainer:
 
         # the fused path's features are encoded once and kept for the 4 epochs
         # (fp16 under autocast: 2^21 rows x 198 x 2 B = 0.8 GB of HBM)
-        manual = self.fused and self.amp and os.environ.get("BGX_PPO_MANUAL", "1") != "0" and _is_policy_mlp(self.net)
+        manual = self.fused and self.amp and _is_policy_mlp(self.net)
         fused_head = manual and _fused_head_ok(self.net)
         # the fused head generates every feature it needs from the records (fc1 forward,
         # gW1); the other paths read features encoded once for the 4 epochs

@@ -42,10 +42,6 @@ __device__ __forceinline__ int initial_byte(int l) {
 // ------------------------------------------------------------------- dice --
 // backgammon_env.py:245-246: np.random.randint(1,7) on numpy's legacy MT19937:
 // x = next_u32 & 7, rejected while x > 5, die = x + 1.
-#ifndef BGX_PHILOX_VALU
-#define BGX_PHILOX_VALU 0
-#endif
-
 struct Rng {
     int mode;                 // BGX_DICE_*
     // MT19937 (per lane, or the shared stream for SHARED mode's serial kernel)
@@ -118,12 +114,6 @@ struct Rng {
         if (b != blkid) {
             uint32_t c0 = (uint32_t)b, c1 = (uint32_t)(b >> 32), c2 = lane, c3 = 0x42474D4Eu;
             uint32_t a0 = k0, a1 = k1;
-#if BGX_PHILOX_VALU
-            // the block (wave-uniform) on the SIMD's vector ALU instead of the CU's one
-            // scalar unit, the env step's busiest pipe: VGPR operands make
-            // the rounds VALU code, readfirstlane brings the words back
-            __asm__ volatile("" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(a0), "+v"(a1));
-#endif
             #pragma unroll
             for (int r = 0; r < 10; ++r) {
                 const uint32_t h0 = __umulhi(0xD2511F53u, c0), l0 = 0xD2511F53u * c0;
@@ -131,9 +121,6 @@ struct Rng {
                 c0 = h1 ^ c1 ^ a0; c1 = l1; c2 = h0 ^ c3 ^ a1; c3 = l0;
                 a0 += 0x9E3779B9u; a1 += 0xBB67AE85u;
             }
-#if BGX_PHILOX_VALU
-            c0 = ufl(c0); c1 = ufl(c1); c2 = ufl(c2); c3 = ufl(c3);
-#endif
             blk0 = c0; blk1 = c1; blk2 = c2; blk3 = c3; blkid = b;
         }
         const uint32_t w = (uint32_t)(ctr & 3u);
@@ -430,11 +417,6 @@ __device__ __forceinline__ void store_rec(const Args& A, int gi, int bv) { A.lan
 // Engine object behind the C ABI's opaque bgx_engine*.
 struct bgx_engine {
     int device;
-    int lds_log;      // 8 .. 11 (the split's doubles prefix; standalone movegen 9 .. 11)
-    int memo_mode;    // 0: none, 1: separate memo tables, 2: memo inside the dedup table
-    int heavy_wpe;    // 5: the doubles prefix held to 5 waves/SIMD (A/B)
-    int tier1_grid;   // workgroups of the step's first overflow tier
-    bool split;       // Philox mode: doubles-prefix launch, then the light launch
     bg::Args a;
     uint4* slow_tables;
     int slow_waves;
@@ -444,11 +426,9 @@ struct bgx_engine {
     // overflow counters, two 16-byte sets: a Philox step uses set `ovf_parity`
     // (Args::ovf_count) and its k_order_count zeroes the other set for the next
     // step, so the step needs no separate memset launch
-    hipStream_t step_side;      // BGX_STEP_OVERLAP: light launch beside the heavy one
+    hipStream_t step_side;      // the light launch beside the heavy one, and the next dispatch order
     hipEvent_t step_ev[4];      // fork, light done, heavy done, dispatch order done
     bool order_pending;         // the next step's launches wait for step_ev[3]
-    int step_overlap;
-    bool order_async;           // BGX_ORDER_ASYNC
     int32_t* ovf_base;
     int ovf_parity;
     bool ovf_next_zeroed;

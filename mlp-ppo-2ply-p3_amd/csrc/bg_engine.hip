@@ -501,12 +501,9 @@ int fail(hipError_t e, int code = BGX_EDEVICE) {
 int bgx_internal_fail(hipError_t e) { return fail(e); }
 
 #define CK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return fail(_e); } while (0)
-#define LAUNCH_LOG(e, K, grid, s, ...)                                                            \
-    do {                                                                                          \
-        if ((e)->lds_log == 9) hipLaunchKernelGGL(K<9>, grid, dim3(64), 0, s, __VA_ARGS__);       \
-        else if ((e)->lds_log == 11) hipLaunchKernelGGL(K<11>, grid, dim3(64), 0, s, __VA_ARGS__); \
-        else hipLaunchKernelGGL(K<10>, grid, dim3(64), 0, s, __VA_ARGS__);                        \
-    } while (0)
+// the per-position kernels (reset, standalone movegen, regeneration) with the
+// 512-slot dedup table
+#define LAUNCH_LOG(e, K, grid, s, ...) hipLaunchKernelGGL(K<9>, grid, dim3(64), 0, s, __VA_ARGS__)
 #define CKL() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return fail(_e); } while (0)
 
 static void launch_order(bgx_engine* e, hipStream_t s) {
@@ -519,41 +516,14 @@ static void launch_order(bgx_engine* e, hipStream_t s) {
     e->perm_valid = true;
 }
 
-static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, const int32_t* actions, float* obs,
-                        float* reward, uint8_t* done, int32_t* info, int base = 0) {
+static void launch_step(hipStream_t s, const Args& a, int grid, const int32_t* actions, float* obs, float* reward,
+                        uint8_t* done, int32_t* info, int base = 0) {
     if (grid <= 0) return;
-#define STEP_K(...) hipLaunchKernelGGL((k_step<__VA_ARGS__>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, \
-                                       info, base)
-    // default (the split's doubles prefix): a 512-slot table and no revisit memo
-    // (8 KB of LDS): the doubles walks that cannot bear off use no table at all,
-    // so occupancy (VGPR-bound, 4 waves/SIMD) beats a bigger table (C3: 1,024
-    // slots + memo 242 M/s, 512 slots + memo inside 284 M/s, no memo 288 M/s)
-    if (e->memo_mode == 2 && e->lds_log == 9) {
-        if (e->heavy_wpe == 5) STEP_K(0, 9, 2, false, 5);
-        else STEP_K(0, 9, 2);
-        return;
-    }
-    if (e->memo_mode == 2 && e->lds_log == 8) { STEP_K(0, 8, 2); return; }
-    if (e->memo_mode == 0) {
-        if (e->lds_log == 8) STEP_K(0, 8, 0);
-        else if (e->heavy_wpe == 4) STEP_K(0, 9, 0, false, 4);
-        else STEP_K(0, 9, 0);
-        return;
-    }
-#undef STEP_K
-    if (e->memo_mode == 2) {
-        if (e->lds_log == 11)
-            hipLaunchKernelGGL((k_step<0, 11, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
-        else if (e->lds_log == 9)
-            hipLaunchKernelGGL((k_step<0, 9, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
-        else
-            hipLaunchKernelGGL((k_step<0, 10, 2>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
-    } else if (e->lds_log == 9)
-        hipLaunchKernelGGL((k_step<0, 9>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
-    else if (e->lds_log == 11)
-        hipLaunchKernelGGL((k_step<0, 11>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
-    else
-        hipLaunchKernelGGL((k_step<0, 10>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
+    // the split's doubles prefix: a 512-slot table and no revisit memo (8 KB of LDS):
+    // the doubles walks that cannot bear off use no table at all, so occupancy
+    // (VGPR-bound, 4 waves/SIMD) beats a bigger table (C3: 1,024 slots + memo 242 M/s,
+    // 512 slots + memo inside 284 M/s, no memo 288 M/s; measured round 2)
+    hipLaunchKernelGGL((k_step<0, 9, 0>), dim3(grid), dim3(64), 0, s, a, actions, obs, reward, done, info, base);
 }
 
 // Doubles share of the dispatch order (Philox mode): the expected doubles
@@ -562,17 +532,18 @@ static void launch_step(bgx_engine* e, hipStream_t s, const Args& a, int grid, c
 // With the XCD-aware order the count is a multiple of 8, so the light launch's
 // blocks keep the order's position -> XCD residue.
 static int heavy_grid(int B, bool xcd) {
-    const char* f = getenv("BGX_HEAVY_FRAC");
-    const double g = f ? atof(f) * B : B / 6.0 + 4.0 * std::sqrt(B * 5.0 / 36.0) + 32.0;
+    const double g = B / 6.0 + 4.0 * std::sqrt(B * 5.0 / 36.0) + 32.0;
     int h = g >= B ? B : (int)g;
     if (xcd) h = (h + 7) & ~7;
     return h > B ? B : h;
 }
 
+constexpr int kTier1Grid = 256;      // workgroups of the step's first overflow tier
+
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
                      const uint8_t* dice, int cap, int16_t* nm, int32_t* nt, uint64_t* moves) {
     if (src == 0) {
-        hipLaunchKernelGGL((k_movegen_over<0, 1>), dim3(e->tier1_grid), dim3(64), 0, s, e->a, boards, players, dice,
+        hipLaunchKernelGGL((k_movegen_over<0, 1>), dim3(kTier1Grid), dim3(64), 0, s, e->a, boards, players, dice,
                            cap, nm, nt, moves, e->slow_tables);
         hipLaunchKernelGGL((k_movegen_over<0, 2>), dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice,
                            cap, nm, nt, moves, e->slow_tables);
@@ -597,22 +568,7 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     memset(&e->a, 0, sizeof e->a);
     e->device = device;
     e->seed = seed;
-    const char* ll = getenv("BGX_LDS_LOG");
-    e->lds_log = ll ? atoi(ll) : 9;
-    if (e->lds_log < 8 || e->lds_log > 11) e->lds_log = 9;
-    const char* hw = getenv("BGX_HEAVY_WPE");
-    e->heavy_wpe = hw ? atoi(hw) : 1;
-    const char* sp = getenv("BGX_SPLIT");
-    e->split = !(sp && sp[0] == '0');
-    const char* sov = getenv("BGX_STEP_OVERLAP");
-    e->step_overlap = sov ? atoi(sov) : 1;
-    const char* oas = getenv("BGX_ORDER_ASYNC");     // "0": dispatch order on the caller's stream (A/B)
-    e->order_async = !(oas && oas[0] == '0');
     e->order_pending = false;
-    const char* t1g = getenv("BGX_TIER1_GRID");      // the step's first overflow tier (A/B)
-    e->tier1_grid = t1g && atoi(t1g) > 0 ? atoi(t1g) : 256;
-    const char* mm = getenv("BGX_MEMO_MODE");
-    e->memo_mode = mm ? atoi(mm) : 0;
     Args& A = e->a;
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
@@ -789,12 +745,8 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
         hipLaunchKernelGGL((k_step<1, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
                            info_dev, 0);
         hipLaunchKernelGGL(k_shared_dice, dim3(1), dim3(64), 0, s, A);
-        if (e->lds_log == 9)
-            hipLaunchKernelGGL((k_step<2, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
-                               info_dev, 0);
-        else
-            hipLaunchKernelGGL((k_step<2, 10>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev,
-                               done_dev, info_dev, 0);
+        hipLaunchKernelGGL((k_step<2, 9>), dim3(A.B), dim3(64), 0, s, A, actions_dev, obs_dev, reward_dev, done_dev,
+                           info_dev, 0);
     } else {
         if (e->order_pending) {              // the previous step's dispatch order (side stream)
             CK(hipStreamWaitEvent(s, e->step_ev[3], 0));
@@ -802,14 +754,14 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
         }
         Args a = A;
         a.perm = e->perm_valid ? e->perm : nullptr;
-        const int heavy = a.perm && e->split ? heavy_grid(A.B, A.xcd != 0) : A.B;
+        const int heavy = a.perm ? heavy_grid(A.B, A.xcd != 0) : A.B;
         // Split dispatch (Philox mode): the predicted-doubles prefix of the order
         // with the big dedup table + revisit memo (26 KB of LDS per wave), then the
         // rest with a 256-slot table, no memo, no doubles code (4 KB, 49 VGPRs: the
         // hardware wave limit, ~5x the resident waves; doubles go to the overflow tiers).
         // Plain stream order -- no cross-stream wait that a serializing tool
         // (profiler) or a shared hardware queue could deadlock.
-        if (e->step_overlap && heavy < A.B) {
+        if (heavy < A.B) {
             // fork-join on events: the light launch runs on a side stream beside
             // the heavy one (filling the CUs its tail leaves idle)
             if (!e->step_side) {
@@ -822,11 +774,10 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
                 hipLaunchKernelGGL((k_step<0, 8, 0, true>), dim3(A.B - heavy), dim3(64), 0, e->step_side, a,
                                    actions_dev, obs_dev, reward_dev, done_dev, info_dev, heavy);
             };
-            if (e->step_overlap == 2) light();
-            launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
-            if (e->step_overlap != 2) light();
+            launch_step(s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+            light();
             CK(hipEventRecord(e->step_ev[1], e->step_side));
-            if (A.cls && e->order_async) {
+            if (A.cls) {
                 // the next dispatch order on the side stream once both launches have
                 // written their classes: it runs beside this stream's overflow tiers
                 // and the caller's next policy kernel instead of before them; the
@@ -839,7 +790,7 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
             }
             CK(hipStreamWaitEvent(s, e->step_ev[1], 0));
         } else {
-            launch_step(e, s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
+            launch_step(s, a, heavy, actions_dev, obs_dev, reward_dev, done_dev, info_dev);
             if (heavy < A.B)
                 hipLaunchKernelGGL((k_step<0, 8, 0, true>), dim3(A.B - heavy), dim3(64), 0, s, a, actions_dev,
                                    obs_dev, reward_dev, done_dev, info_dev, heavy);

@@ -25,11 +25,10 @@
 #include <stdlib.h>
 #include "../../include/bgx.h"
 
-#ifndef BGX_POLICY_W1_AHEAD
-#define BGX_POLICY_W1_AHEAD 2      // k-blocks of W1 fragments in flight in the policy kernel's GEMM1
-#endif
 
 namespace {
+
+constexpr int kW1Ahead = 2;      // k-blocks of W1 fragments in flight in the policy kernel's GEMM1
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -270,7 +269,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
         for (int r = 0; r < 16; ++r) x1[t][r] = b1p[(t * 16 + r) * 64 + l];
     // W1's fragments stream from L2 kPD k-blocks ahead of their MFMAs (a ring of
     // registers): at one or two waves per SIMD nothing else hides the L2 latency
-    constexpr int kPD = BGX_POLICY_W1_AHEAD;
+    constexpr int kPD = kW1Ahead;
     uint4 wf[kPD + 1][2 * T];
     #pragma unroll
     for (int p = 0; p < kPD; ++p)

@@ -43,24 +43,11 @@
 
 using namespace bg;
 
-// evaluator build knobs (A/B: tools/build_variant.sh + tools/ab_eval.sh)
-#ifndef BGX_EVAL_WIDE_WAVES
-#define BGX_EVAL_WIDE_WAVES 8
-#endif
-#ifndef BGX_EVAL_PIPE
-#define BGX_EVAL_PIPE 0
-#endif
-#ifndef BGX_EVAL_SKIP
-#define BGX_EVAL_SKIP 0
-#endif
-#ifndef BGX_EVAL_NARROW_WAVES
-#define BGX_EVAL_NARROW_WAVES 4
-#endif
-
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kEvalWideWaves = 8, kEvalNarrowWaves = 4;   // waves per LDS-weight evaluator workgroup
 constexpr int kKB = 13;            // 208 / 16 k-steps of v_mfma_f32_32x32x16_f16
 constexpr int kSlowQueue = 1 << 20;
 constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
@@ -690,6 +677,19 @@ __device__ __forceinline__ f16x8 feat16(const Leaf& L, int kb, int h) {
     return __builtin_bit_cast(f16x8, v);
 }
 
+// feat16 with the point units read from a 256-entry LDS table instead of computed:
+// utab[b] = units_pair(b), the B-operand half-block of a point pair whose counts are
+// the two nibbles of byte b.  One ds_read_b128 replaces ~10 VALU per k-block and leaf
+// tile (the register-weight evaluators are otherwise VALU-issue-bound: 9 VALU per MFMA
+// at H = 40).
+__device__ __forceinline__ void build_unit_table(uint4* utab) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) utab[b] = units_pair((uint32_t)b);
+}
+__device__ __forceinline__ f16x8 feat16t(const Leaf& L, int kb, int h, const uint4* utab) {
+    if (kb < 12) return __builtin_bit_cast(f16x8, utab[kb_byte(L, kb, h)]);
+    return feat16(L, kb, h);
+}
+
 __device__ __forceinline__ int ord_f32(float v) {
     const int b = __float_as_int(v);
     return b >= 0 ? b : b ^ 0x7FFFFFFF;
@@ -763,67 +763,19 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
     #pragma unroll 1
     for (int g0 = 0; g0 < NT; g0 += G) {
         f32x16 x[2][G];
-#if BGX_EVAL_PIPE
-        // the next k-block's weight fragments are read while this k-block's MFMAs run
-        // (LLVM otherwise issues each ds_read_b128 one or two MFMAs before its use and
-        // the wave waits on lgkmcnt; sched_barrier pins the order)
-        uint4 abuf[G], nbuf[G];
-        #pragma unroll
-        for (int t = 0; t < G; ++t) abuf[t] = g0 + t < NT ? wq[(g0 + t) * 64 + l + z] : make_uint4(0, 0, 0, 0);
-#endif
-#if BGX_EVAL_SKIP
-        #pragma unroll
-        for (int n = 0; n < 2; ++n)
-            #pragma unroll
-            for (int t = 0; t < G; ++t) x[n][t] = (f32x16){};
-#endif
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) {
-#if BGX_EVAL_PIPE
-            if (kb + 1 < kKB) {
-                #pragma unroll
-                for (int t = 0; t < G; ++t)
-                    if (g0 + t < NT) nbuf[t] = wq[((kb + 1) * NT + g0 + t) * 64 + l + z];
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#endif
             const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
-#if BGX_EVAL_SKIP
-            // exact: a k-block whose 4 points are empty in all 32 leaves of a tile has
-            // all-zero features there, and its products add exactly 0 to the
-            // accumulators (finite weights).  Leaves of a tile share their job's root
-            // afterstate, so whole 4-point groups are often empty (mean 4 of 12 per board)
-            const bool on0 = kb >= 12 || __ballot(kb_byte(L[0], kb < 12 ? kb : 0, h) != 0u) != 0ull;
-            const bool on1 = kb >= 12 || __ballot(kb_byte(L[1], kb < 12 ? kb : 0, h) != 0u) != 0ull;
-#else
-            const bool on0 = true, on1 = true;
-#endif
             #pragma unroll
             for (int t = 0; t < G; ++t) {
                 if (g0 + t < NT) {
-#if BGX_EVAL_PIPE
-                    const f16x8 a = __builtin_bit_cast(f16x8, abuf[t]);
-#else
                     const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + g0 + t) * 64 + l + z]);
-#endif
-#if BGX_EVAL_SKIP
-                    if (on0) x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, x[0][t], 0, 0, 0);
-                    if (on1) x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, x[1][t], 0, 0, 0);
-#else
-                    (void)on0; (void)on1;
                     const f32x16 c0 = kb == 0 ? (f32x16){} : x[0][t];
                     const f32x16 c1 = kb == 0 ? (f32x16){} : x[1][t];
                     x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f0, c0, 0, 0, 0);
                     x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f1, c1, 0, 0, 0);
-#endif
                 }
             }
-#if BGX_EVAL_PIPE
-            if (kb + 1 < kKB) {
-                #pragma unroll
-                for (int t = 0; t < G; ++t) abuf[t] = nbuf[t];
-            }
-#endif
         }
         #pragma unroll
         for (int n = 0; n < 2; ++n)
@@ -845,7 +797,7 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
 // several workgroups per CU) or 8 waves (H = 128: 120 KiB, one workgroup per CU,
 // two waves per SIMD)
 template <int NT> struct EvalShape {
-    static constexpr int kWaves = NT <= 4 ? BGX_EVAL_NARROW_WAVES : BGX_EVAL_WIDE_WAVES;
+    static constexpr int kWaves = NT <= 4 ? kEvalNarrowWaves : kEvalWideWaves;
 };
 
 template <int NT>
@@ -929,6 +881,9 @@ void k_eval_rw_wide(EvalArgs E) {
     static_assert(wide_tiles(NT), "wide form");
     constexpr int NW = slices(NT) / 2, NS = slices(NT);
     __shared__ float part[2][NW][64];
+    __shared__ uint4 utab[256];
+    build_unit_table(utab);
+    __syncthreads();
     const int l = lane_id(), h = l >> 5, c = l & 31, wv = threadIdx.x >> 6;
     uint4 wh[kKB], wl[kKB];
     #pragma unroll
@@ -958,7 +913,7 @@ void k_eval_rw_wide(EvalArgs E) {
         f32x16 x0, x1;
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) {
-            const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
+            const f16x8 f0 = feat16t(L[0], kb, h, utab), f1 = feat16t(L[1], kb, h, utab);
             const f16x8 ah = __builtin_bit_cast(f16x8, wh[kb]), al = __builtin_bit_cast(f16x8, wl[kb]);
             x0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, kb == 0 ? (f32x16){} : x0, 0, 0, 0);
             x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f1, kb == 0 ? (f32x16){} : x1, 0, 0, 0);
@@ -1002,7 +957,9 @@ template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_eval_rw_narrow(EvalArgs E) {
     static_assert(NT <= 3, "narrow register form: at most 3 tiles (156 VGPRs of weights)");
     __shared__ float wvs[NT * 8 * 64];
+    __shared__ uint4 utab[256];
     for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = E.wvq[i];
+    build_unit_table(utab);
     __syncthreads();
     const int l = lane_id(), h = l >> 5, c = l & 31;
     uint4 wq[NT][kKB];
@@ -1020,25 +977,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (; tile < tiles; tile += stride) {
         const Leaf L = make_leaf(raw, row);
         const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
-        raw = load_raw(E, nxt * 32 + c);
         f32x16 x[NT];
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) {
-            const f16x8 f = feat16(L, kb, h);
+            const f16x8 f = feat16t(L, kb, h, utab);
             #pragma unroll
             for (int t = 0; t < NT; ++t)
                 x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wq[t][kb]), f,
                                                               kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+            if (kb == 6) raw = load_raw(E, nxt * 32 + c);   // the next tile's entries, mid-loop (registers)
         }
         row = load_row(E, raw);
-        float v = 0.0f;
+        // hi + lo, relu, times the head weights: two units per packed-fp32 add / fma
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        f32x2 v2 = {0.0f, 0.0f};
         #pragma unroll
         for (int t = 0; t < NT; ++t)
             #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < 8; j += 2) {
                 const int r = j < 4 ? j : j + 4;
-                v = fmaf(fmaxf(x[t][r] + x[t][r + 4], 0.0f), wvs[(t * 8 + j) * 64 + l], v);
+                f32x2 u = f32x2{x[t][r], x[t][r + 1]} + f32x2{x[t][r + 4], x[t][r + 5]};
+                u.x = fmaxf(u.x, 0.0f);
+                u.y = fmaxf(u.y, 0.0f);
+                v2 = __builtin_elementwise_fma(u, f32x2{wvs[(t * 8 + j) * 64 + l], wvs[(t * 8 + j + 1) * 64 + l]}, v2);
             }
+        float v = v2.x + v2.y;
         v += __shfl_xor(v, 32) + E.bv;
         const int jb = L.job;
         float vv = L.valid ? v : INFINITY;
@@ -1256,15 +1219,24 @@ static int persistent_grid(const bgx_engine* e, K kernel, int per_cu_cap) {
 
 typedef void (*EvalFn)(EvalArgs);
 typedef void (*EvalRowsFn)(EvalRowsArgs);
+static int eval_waves(int NT) { return NT <= 4 ? kEvalNarrowWaves : kEvalWideWaves; }
 // the 2-ply evaluator for NT 16-unit slices and its workgroup size: W1 in registers
 // (k_eval_rw_*) except at NT = 4 (208 VGPRs of weights in one wave; LDS weights)
 struct EvalPick { EvalFn fn; int threads; };
 static EvalPick eval_kernel(int NT) {
+    if (const char* f = getenv("BGX_EVAL_FORM"); f && f[0] == 'l') {      // A/B: the LDS-weight form
+        switch (NT) {
+            case 1: return {k_eval<1>, 64 * eval_waves(1)}; case 2: return {k_eval<2>, 64 * eval_waves(2)};
+            case 3: return {k_eval<3>, 64 * eval_waves(3)}; case 4: return {k_eval<4>, 64 * eval_waves(4)};
+            case 5: return {k_eval<5>, 64 * eval_waves(5)}; case 6: return {k_eval<6>, 64 * eval_waves(6)};
+            case 7: return {k_eval<7>, 64 * eval_waves(7)}; default: return {k_eval<8>, 64 * eval_waves(8)};
+        }
+    }
     switch (NT) {
         case 1: return {k_eval_rw_narrow<1>, 256};
         case 2: return {k_eval_rw_narrow<2>, 256};
         case 3: return {k_eval_rw_narrow<3>, 256};
-        case 4: return {k_eval<4>, 64 * BGX_EVAL_NARROW_WAVES};
+        case 4: return {k_eval<4>, 64 * kEvalNarrowWaves};
         case 5: return {k_eval_rw_wide<5>, 64 * (slices(5) / 2)};
         case 6: return {k_eval_rw_wide<6>, 64 * (slices(6) / 2)};
         case 7: return {k_eval_rw_wide<7>, 64 * (slices(7) / 2)};
@@ -1279,7 +1251,6 @@ static EvalRowsFn eval_rows_kernel(int NT) {
     }
 }
 // the launch's workgroup size must be the kernels' EvalShape<NT>::kWaves (their tile stride)
-static int eval_waves(int NT) { return NT <= 4 ? BGX_EVAL_NARROW_WAVES : BGX_EVAL_WIDE_WAVES; }
 
 // resident workgroups of an evaluator over the whole device
 template <typename K>
@@ -1429,27 +1400,20 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         S2 S{rowrec, 0, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
              retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>(), 3, 3};
-        if (const char* v = getenv("BGX_2PLY_MEMO")) S.memo_mask = atoi(v);
-        if (const char* v = getenv("BGX_2PLY_MEMO_SHARE")) S.memo_share = atoi(v);
-        // doubles enumerator: dedup table 2^LOG slots + revisit memo kind (BGX_2PLY_HEAVY=LOG:MK)
-        int hlog = 9, hmk = 2, hwpe = 0;
+        // doubles enumerator: 512-slot dedup table with the revisit memo inside it, held to
+        // 128 VGPRs (4 waves/SIMD, +1.5 %).  Tests (BGX_2PLY_HEAVY = 9:0 / 10:0) run the
+        // exact alternatives without the memo (9:0) or with a 1,024-slot table (10:0): the
+        // same leaves, Q and choices (tests/test_gpu_search.py)
+        int hlog = 9, hmk = 2;
         if (const char* hv = getenv("BGX_2PLY_HEAVY")) {
             hlog = atoi(hv);
             const char* c = strchr(hv, ':');
-            if (c) { hmk = atoi(c + 1); c = strchr(c + 1, ':'); if (c) hwpe = atoi(c + 1); }
+            hmk = c ? atoi(c + 1) : 2;
         }
-        // occupancy floor: <= 128 VGPRs (4 waves/SIMD) for the doubles walk (+1.5 %)
         void (*kheavy)(S2) = k_enum<9, 2, 1, 4>;
         void (*klist)(S2) = k_enum<9, 2, 2, 4>;
         if (hlog == 9 && hmk == 0) { kheavy = k_enum<9, 0, 1>; klist = k_enum<9, 0, 2>; }
-        else if (hlog == 9 && hmk == 2 && hwpe == 1) { kheavy = k_enum<9, 2, 1, 1>; klist = k_enum<9, 2, 2, 1>; }
-        else if (hlog == 9 && hmk == 2 && hwpe == 5) { kheavy = k_enum<9, 2, 1, 5>; klist = k_enum<9, 2, 2, 5>; }
-        else if (hlog == 9 && hmk == 2 && hwpe == 6) { kheavy = k_enum<9, 2, 1, 6>; klist = k_enum<9, 2, 2, 6>; }
-        else if (hlog == 8 && hmk == 2) { kheavy = k_enum<8, 2, 1>; klist = k_enum<8, 2, 2>; }
-        else if (hlog == 8 && hmk == 0) { kheavy = k_enum<8, 0, 1>; klist = k_enum<8, 0, 2>; }
         else if (hlog == 10 && hmk == 0) { kheavy = k_enum<10, 0, 1>; klist = k_enum<10, 0, 2>; }
-        else if (hlog == 9 && hmk == 1) { kheavy = k_enum<9, 1, 1>; klist = k_enum<9, 1, 2>; }
-        else if (hlog == 10 && hmk == 2) { kheavy = k_enum<10, 2, 1>; klist = k_enum<10, 2, 2>; }
         else { hlog = 9; hmk = 2; }
         S.cap_heavy = (7 << hlog) / 8;
         if (const char* fs = getenv("BGX_2PLY_LDS_CAP")) {    // tests: force the overflow tiers ("first[:mid]")
@@ -1462,20 +1426,10 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    (const uint4*)(f16s + 4), f16s + 4 + kKB * slices(NT) * 64 * 4, value_bias};
         // the non-doubles enumerator: the row-level walk held to 80 VGPRs (6 waves/SIMD,
-        // +1.2 % over its natural 91).  A/B: BGX_2PLY_ROWS=0 the per-job walk only;
-        // BGX_2PLY_LWPE=1 the row-level walk without the floor, =8 the per-job walk
-        // held to 64 VGPRs (it spills and runs slower)
-        const char* lw = getenv("BGX_2PLY_LWPE");
-        const char* rw = getenv("BGX_2PLY_ROWS");
-        void (*klight)(S2) = lw && atoi(lw) == 8 ? k_enum<kLogLight, -1, 0, 8>
-                             : lw && atoi(lw) == 7 ? k_enum<kLogLight, -1, 3, 7>
-                             : lw && atoi(lw) == 9 ? k_enum<kLogLight, -1, 3, 8>
-                             : (rw && rw[0] == '0') ? k_enum<kLogLight, -1, 0, 1>
-                             : (lw && atoi(lw) == 1) ? k_enum<kLogLight, -1, 3, 1> : k_enum<kLogLight, -1, 3, 6>;
-        int g_light = persistent_grid(e, klight, 32);
-        int g_heavy = persistent_grid(e, kheavy, 32);
-        if (const char* v = getenv("BGX_2PLY_HGRID")) g_heavy = atoi(v) > 0 ? atoi(v) : g_heavy;
-        if (const char* v = getenv("BGX_2PLY_LGRID")) g_light = atoi(v) > 0 ? atoi(v) : g_light;
+        // +1.2 % over its natural 91)
+        void (*klight)(S2) = k_enum<kLogLight, -1, 3, 6>;
+        const int g_light = persistent_grid(e, klight, 32);
+        const int g_heavy = persistent_grid(e, kheavy, 32);
         const int g_list = persistent_grid(e, klist, 32);
         const int g_t0 = persistent_grid(e, k_enum_tier<10, 0>, 32);
         const int g_mid = persistent_grid(e, k_enum_tier<kLogMid, 1>, 32);
@@ -1508,17 +1462,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         const int g_eval = occ_eval * persistent_grid(e, keval.fn, 1);     // resident workgroups
         if (!e->search_ev[0])
             for (hipEvent_t& ev : e->search_ev) SCK(hipEventCreate(&ev));
-        const char* ov = getenv("BGX_2PLY_OVERLAP");    // "0": enumerators back to back (A/B)
-        const bool overlap = !(ov && ov[0] == '0');
-        if (overlap && !e->search_side) {
-            // BGX_2PLY_SIDE_PRIO = hi / lo: the non-doubles enumerator's stream priority (A/B)
-            const char* pr = getenv("BGX_2PLY_SIDE_PRIO");
-            int lo = 0, hi = 0;
-            if (pr && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && (pr[0] == 'h' || pr[0] == 'l'))
-                SCK(hipStreamCreateWithPriority(&e->search_side, hipStreamNonBlocking, pr[0] == 'h' ? hi : lo));
-            else
-                SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
-        }
+        if (!e->search_side) SCK(hipStreamCreateWithFlags(&e->search_side, hipStreamNonBlocking));
         SCK(hipEventRecord(e->search_ev[0], s));
         auto eval = [&](hipStream_t st) {
             hipLaunchKernelGGL(keval.fn, dim3(g_eval), dim3(keval.threads), 0, st, E);
@@ -1533,18 +1477,13 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             hipLaunchKernelGGL(k_enum_slow, dim3(g(e->slow_waves)), dim3(64), 0, s, S, e->slow_tables);
         };
         for (int round = 0;; ++round) {
-            if (round == 0) {
-                if (overlap) {       // the non-doubles enumerator beside the doubles one
-                    SCK(hipEventRecord(e->search_ev[3], s));
-                    SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
-                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                    hipLaunchKernelGGL(klight, dim3(g_light), dim3(64), 0, e->search_side, S);
-                    SCK(hipEventRecord(e->search_ev[4], e->search_side));
-                    SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
-                } else {
-                    hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
-                    hipLaunchKernelGGL(klight, dim3(g_light), dim3(64), 0, s, S);
-                }
+            if (round == 0) {       // the non-doubles enumerator beside the doubles one
+                SCK(hipEventRecord(e->search_ev[3], s));
+                SCK(hipStreamWaitEvent(e->search_side, e->search_ev[3], 0));
+                hipLaunchKernelGGL(kheavy, dim3(g_heavy), dim3(64), 0, s, S);
+                hipLaunchKernelGGL(klight, dim3(g_light), dim3(64), 0, e->search_side, S);
+                SCK(hipEventRecord(e->search_ev[4], e->search_side));
+                SCK(hipStreamWaitEvent(s, e->search_ev[4], 0));
                 tiers();
                 SCK(hipEventRecord(e->search_ev[1], s));
                 eval(s);

@@ -10,6 +10,7 @@ tr.rollout()
 torch.cuda.synchronize()
 ts = []
 for _ in range(int(os.environ.get("N", "4"))):
+    time.sleep(0.05)                  # an idle gap that separates the updates in a kernel trace
     t0 = time.perf_counter()
     m = tr.update()
     torch.cuda.synchronize()

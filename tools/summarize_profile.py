@@ -155,7 +155,7 @@ if sq:
 mrows, erows = pmc_rows("mfma"), pmc_rows("efetch")
 evals = []
 for k in kernels:
-    if "k_eval<" not in k["name"]:
+    if not short(k["name"]).startswith("k_eval") or short(k["name"]).startswith("k_eval_rows"):
         continue
     e = {"kernel": short(k["name"]), "avg_ns": k["avg_ns"], "calls": k["calls"]}
     m = mrows.get(k["name"], {})
@@ -174,22 +174,79 @@ for k in kernels:
         e["hbm_read_bytes"] = 2 * statistics.mean(f) * 1024
     evals.append(e)
 
+# ------------------------------------------------- C3 policy kernel (round 4) --
+# k_policy_act on the C3 step (the pol1 / pol2 passes run the PMC command): per
+# dispatch means of its counters; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1,024 SIMDs x
+# its duration x 2.4 GHz); VALU issue = SQ_INSTS_VALU x 2 cycles / the same; the
+# wave-time split from the quad-cycle counters (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY
+# = WAVE_CYCLES).  The duration is the kernel-trace average of its C3 dispatches.
+def merged(kinds, pred):
+    res = {}
+    for kind in kinds:
+        for n, v in pmc_rows(kind).items():
+            if pred(short(n)):
+                d = res.setdefault(short(n), {})
+                for c, vals in v.items():
+                    d.setdefault(c, vals)
+    return res
+
+
+def wave_split(m):
+    wc = statistics.mean(m["SQ_WAVE_CYCLES"]) if "SQ_WAVE_CYCLES" in m else 0
+    if not wc:
+        return None
+    f = lambda c: statistics.mean(m[c]) / wc if c in m else None
+    return {"active_any": f("SQ_ACTIVE_INST_ANY"), "wait_any (s_waitcnt / barrier)": f("SQ_WAIT_ANY"),
+            "wait_inst_any (issue stall)": f("SQ_WAIT_INST_ANY"), "wait_inst_lds": f("SQ_WAIT_INST_LDS"),
+            "active_lds": f("SQ_ACTIVE_INST_LDS"), "active_valu": f("SQ_ACTIVE_INST_VALU")}
+
+
+policy = []
+for name, m in merged(("pol1", "pol2"), lambda n: n.startswith("k_policy_act")).items():
+    kk = next((k for k in kernels if short(k["name"]) == name), None)
+    if not kk:
+        continue
+    rows = [r for r in trace if short(r["Kernel_Name"]) == name]
+    gmax = max(int(r["Grid_Size_X"]) for r in rows)
+    dur = statistics.mean([int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
+                           if int(r["Grid_Size_X"]) * 4 >= gmax])
+    e = {"kernel": name, "avg_ns_c3": dur, "counters_per_dispatch": {c: statistics.mean(v) for c, v in m.items()}}
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+        e["mfma_busy_frac_at_2p4GHz"] = statistics.mean(m["SQ_VALU_MFMA_BUSY_CYCLES"]) / (SIMDS * dur * CLOCK_GHZ)
+    if "SQ_INSTS_VALU" in m:
+        e["valu_issue_frac_at_2p4GHz"] = statistics.mean(m["SQ_INSTS_VALU"]) * 2 / (SIMDS * dur * CLOCK_GHZ)
+    e["wave_time_split"] = wave_split(m)
+    policy.append(e)
+
+# ------------------------------------------------ 2-ply enumerators (round 4) --
+# per enumerator kernel: dispatch count, instruction totals and per-wave figures, the
+# wave-time split (enum1 / enum2 passes, the 2-ply command), and the kernel-trace time
+enums = []
+for name, m in merged(("enum1", "enum2"), lambda n: n.startswith("k_enum")).items():
+    kk = next((k for k in kernels if short(k["name"]) == name), None)
+    e = {"kernel": name, "dispatches": len(next(iter(m.values()))),
+         "totals": {c: sum(v) for c, v in m.items()},
+         "avg_ns": kk["avg_ns"] if kk else None, "calls": kk["calls"] if kk else None,
+         "wave_time_split": wave_split(m)}
+    enums.append(e)
+
 # per-pass, per-kernel counter totals and dispatch counts (the raw CSVs reduced, so the
 # figures above can be recomputed from what is committed under profiles/)
 with open(os.path.join(out, "pmc_totals.csv"), "w") as fo:
     fo.write("pass,kernel,counter,dispatches,total\n")
-    for kind in ("fetch", "write", "sqi", "sqc", "mfma", "efetch"):
+    for kind in ("fetch", "write", "sqi", "sqc", "mfma", "efetch", "pol1", "pol2", "enum1", "enum2"):
         for n, v in pmc_rows(kind).items():
             for c, vals in v.items():
                 fo.write(f"{kind},{short(n).replace(',', ';')},{c},{len(vals)},{sum(vals):.17g}\n")
 
 summary = {"command": "python bench.py " + cmd, "pmc_command": "python bench.py " + pmc_cmd,
-           "kernels": kernels[:24], "env_step": env, "two_ply_eval": evals}
+           "kernels": kernels[:24], "env_step": env, "two_ply_eval": evals, "policy": policy,
+           "two_ply_enum": enums}
 json.dump(summary, open(os.path.join(out, "summary.json"), "w"), indent=1)
 for k in kernels[:24]:
     print(f"{k['pct']:6.2f}% {k['avg_ns']/1e3:10.1f} us (tail {k.get('avg_ns_timed_tail', 0)/1e3:.1f}) "
           f"x{k['calls']:4d}  {k['name'][:70]}  {k.get('hbm_bytes_per_launch', 0)/1e6:.1f} MB")
 if "sq" in env:
     print(json.dumps(env["sq"], indent=1))
-for e in evals:
+for e in evals + policy + enums:
     print(json.dumps(e))
