@@ -358,6 +358,28 @@ def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
                                  f"{units}/{hidden} ({tiles}) x 208/198 (K padding, bias as a feature)"}}
 
 
+def policy_roofline(pairs, rows: int, prof, src) -> dict:
+    """C3's policy kernel (k_policy_act: encoder + 198->128->{500,1} MLP on split-f16 MFMA +
+    masked log-softmax + Gumbel-max sample) priced against the dense MFMA peak: algorithmic
+    FLOPs per row 2(198*128 + 128*501) over its HIP-event time per shard launch (eager steps
+    after the timed region, the policy launch of each shard step).  The committed PMC passes
+    of the same kernel (tools/profile.sh pol1/pol2 -> profiles/latest_summary.json "policy")
+    give what the hardware issued: MFMA busy and VALU issue fractions, wave-time split."""
+    ms = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs)
+    flop_row = 2 * (198 * 128 + 128 * 501)
+    ach = rows * flop_row / (ms * 1e-3) / 1e12
+    out = {"kernel": "k_policy_act<4,0> (one 32-row wave per MFMA tile column, rollout specialisation)",
+           "bound": "mfma", "achieved": ach, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": ach / BF16_PEAK_TFLOPS, "flop_per_row": flop_row, "rows_per_launch": rows, "kernel_ms": ms}
+    if prof:
+        p = prof[0]
+        out["pmc"] = {"mfma_busy_frac": p.get("mfma_busy_frac_at_2p4GHz"),
+                      "valu_issue_frac": p.get("valu_issue_frac_at_2p4GHz"),
+                      "wave_time_split": p.get("wave_time_split"), "avg_ns_profiled": p.get("avg_ns_c3"),
+                      "source": "profiles/latest_summary.json policy (" + str(src) + ")"}
+    return out
+
+
 def issue_roofline(sq: dict, lanes: int, kern_ms: float, src) -> dict:
     """The env step's real bound: instruction issue, not HBM.  Wave-instructions per
     lane-step by pipe (SQ_INSTS_* of the C3 step alone, profiles/latest_summary.json,
@@ -426,7 +448,7 @@ def main():
     copy_streams = [torch.cuda.Stream(dev) for _ in range(S)] if want_mirror else None
     counts = [torch.empty(Bs, dtype=torch.int16, device=dev) for _ in range(S)]
     gen = torch.Generator(device=dev).manual_seed(99 + rank)
-    ev_pairs = []
+    ev_pairs, pol_pairs = [], []
     state = {"i": 0, "mirror": args.host_mirror}
 
     def shard_step(k, i, timed):
@@ -446,9 +468,14 @@ def main():
             b, slot = bufs[k], i % ring
             # fused HIP policy step on the engine's lane records in place; it also
             # stores them (int8 boards, no fp32 obs round trip) as the rollout row
+            if timed:
+                p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                p0.record(st)
             net.act(e, seed=4242 + rank * 16 + k, step=i,
                     out=(b["act"][slot], b["logp"][slot], b["value"][slot]), records_out=b["records"][slot])
             if timed:
+                p1.record(st)
+                pol_pairs.append((p0, p1))
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(st)
             e.step(b["act"][slot], want_obs=False, want_info=False, out=(b["reward"][slot], b["done"][slot]))
@@ -559,11 +586,12 @@ def main():
     # passes (tools/profile.sh -> profiles/latest_summary.json; (FETCH_SIZE + WRITE_SIZE)
     # x 1024: the step's 64-B record / 4-8-B scalar reads are single 64-B requests that
     # FETCH_SIZE counts exactly, calibrated in profiles/r2_fetch_calibration.json)
-    traffic, traffic_src, prof_kernels, sq = None, None, None, None
+    traffic, traffic_src, prof_kernels, sq, summ, prof_ok = None, None, None, None, None, False
     prof = os.path.join(ROOT, "profiles", "latest_summary.json")
     if os.path.exists(prof):
         try:
             summ = json.load(open(prof))
+            prof_ok = True
             env = summ.get("env_step")
             if env and env["hbm_bytes_per_step"] > 0:
                 traffic, traffic_src = env["hbm_bytes_per_step"], summ.get("command")
@@ -679,6 +707,9 @@ def main():
             mirror.update(eager)
             mirror["form"] = "eager launches, one copy launch (6 fields) per step and shard"
         line["host_mirror"] = mirror
+    if pol_pairs:
+        line["roofline_policy"] = policy_roofline(pol_pairs, Bs, (summ or {}).get("policy") if prof_ok else None,
+                                                  (summ or {}).get("pmc_command") if prof_ok else None)
     if sq and sq.get("instructions_per_lane_step") and args.workload == "c3":
         line["roofline_issue"] = issue_roofline(sq, Bs, kern_ms, summ.get("pmc_command"))
     if args.two_ply_batches > 0:

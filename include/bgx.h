@@ -289,6 +289,11 @@ int bgx_fc1_packed_size(int32_t hidden);
 int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* stream);
 int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_dev, const void* b1h_dev,
                     int32_t hidden, void* h_dev, void* stream);
+/* bgx_fc1_records that also raises *hmax2_dev (fp32, device; may be NULL) to the
+ * largest |h_row|^2 of its rows (the bound PPOTrainer checks for the fused head's
+ * masked-action shortcut, bgx_ppo_rows). */
+int bgx_fc1_records_ex(const uint8_t* records_dev, int32_t n, const void* packed_dev, const void* b1h_dev,
+                       int32_t hidden, void* h_dev, float* hmax2_dev, void* stream);
 
 /* The fp16 epoch's output layer + loss head without materialised logits
  * (csrc/bg_ppo_fused.hip; replaces, inside ppo_agent.py:268-305 under autocast,
@@ -337,6 +342,12 @@ int bgx_ppo_gw2(const void* h_dev, const int32_t* perm_dev, const void* stats_de
 int64_t bgx_ppo_gw1_workspace(int32_t m);
 int bgx_ppo_gw1(const void* dh_dev, const uint8_t* records_dev, int32_t m, int32_t hidden, float* workspace_dev,
                 float* gw1_dev, void* stream);
+
+/* Discounted returns of a [T][B] rollout per game lane (the reference's
+ * compute_returns, ppo_agent.py:206-216, restated per lane: R_t = r_t + gamma R_{t+1},
+ * reset where done): out [T][B] fp32, the same fp32 roundings as r + gamma * R. */
+int bgx_lane_returns(const float* rewards_dev, const uint8_t* dones_dev, int32_t T, int32_t B, float gamma,
+                     float* out_dev, void* stream);
 
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf

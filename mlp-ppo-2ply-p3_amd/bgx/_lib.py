@@ -63,6 +63,7 @@ SIGNATURES = {
     "bgx_fc1_packed_size": (ctypes.c_int, [_I32]),
     "bgx_fc1_pack": (ctypes.c_int, [_P, _I32, _P, _P]),
     "bgx_fc1_records": (ctypes.c_int, [_P, _I32, _P, _P, _I32, _P, _P]),
+    "bgx_fc1_records_ex": (ctypes.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P]),
     "bgx_ppo_rows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, ctypes.c_float,
                                     ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _I32, _P]),
     "bgx_ppo_gw2_workspace": (ctypes.c_int64, [_I32]),
@@ -71,6 +72,7 @@ SIGNATURES = {
     "bgx_ppo_gw1": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P]),
     "bgx_copy_regions": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "bgx_host_device_ptr": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    "bgx_lane_returns": (ctypes.c_int, [_P, _P, _I32, _I32, ctypes.c_float, _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),
 }

@@ -60,7 +60,22 @@ from .ppo import (EPS_CLIP, GAMMA, LEARNING_RATE, NUM_EPOCHS, VALUE_LOSS_COEF, E
 
 
 def lane_returns(rewards: torch.Tensor, dones: torch.Tensor, gamma: float = GAMMA) -> torch.Tensor:
-    """R_t = r_t + gamma * R_{t+1}, reset at done, per lane; [T, B] (vectorised over B)."""
+    """R_t = r_t + gamma * R_{t+1}, reset at done, per lane; [T, B].  On the GPU one HIP
+    kernel (bgx_lane_returns, the same fp32 roundings as the torch loop below, which
+    stays as the CPU path and the tests' reference)."""
+    if rewards.is_cuda and rewards.dtype == torch.float32 and dones.dtype == torch.uint8:
+        r, d = rewards.contiguous(), dones.contiguous()
+        out = torch.empty_like(r)
+        T, B = r.shape[0], r[0].numel()
+        check(_lib.load().bgx_lane_returns(ctypes.c_void_p(r.data_ptr()), ctypes.c_void_p(d.data_ptr()), T, B,
+                                           float(gamma), ctypes.c_void_p(out.data_ptr()),
+                                           ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream)),
+              "bgx_lane_returns")
+        return out
+    return _lane_returns_torch(rewards, dones, gamma)
+
+
+def _lane_returns_torch(rewards: torch.Tensor, dones: torch.Tensor, gamma: float = GAMMA) -> torch.Tensor:
     T = rewards.shape[0]
     out = torch.empty_like(rewards)
     R = torch.zeros_like(rewards[0])
@@ -177,7 +192,8 @@ class _PPOHead(torch.autograd.Function):
 
 
 def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_coef: float, group=None,
-              amp: bool = True, fused: bool | None = None, step: bool = True, sync: bool = True):
+              amp: bool = True, fused: bool | None = None, step: bool = True, sync: bool = True, guard=None,
+              fused_head: bool = True):
     """One full-batch PPO epoch (ppo_agent.py:268-305) over `chunks` =
     iterable of (features, legal_mask, actions, old_logp, returns, advantages
     [, records]), with gradient accumulation and one all-reduce.  Returns loss
@@ -191,7 +207,8 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
     if fused is None:
         fused = dev_type == "cuda"
     if fused:
-        return _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync)
+        return _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync, guard,
+                                fused_head)
     for feats, legal, actions, old_logp, returns, adv, *_ in chunks:
         w = feats.shape[0] / n_total
         with autocast(device_type=dev_type, enabled=amp):
@@ -364,7 +381,21 @@ def _fused_head_ok(net) -> bool:
     return net.fc1.out_features == 128 and net.action_head.out_features == 500
 
 
-def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
+# The fused head computes, for a row with cnt >= 1 legal actions, only the action tiles
+# holding its legal columns: the masked logits z + log(1e-45) (ppo_agent.py:166) are left
+# out of the log-sum-exp and their gradients are 0.  That equals the reference exactly
+# while every masked term lies e^-30 below the row's sum, i.e. while 2U + log(1e-45) <
+# -30 with U a bound on |z|: U = max_a |Wa_h[a]| max_row |h| + max_a |ba_h[a]|.  The fc1
+# kernel reports max_row |h|^2 (bgx_fc1_records_ex); PPOTrainer checks the bound after
+# each update and redoes an update that broke it on the exact round-2 epoch.
+MASK_SHORTCUT_LIMIT = -MASK_LOG - 30.0
+
+
+def _ptr_or_none(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
     """The fp16-autocast epoch with the output layer and loss head fused
     (bgx_ppo_rows + bgx_ppo_gw2): fc1 from the records (bgx_fc1_records), then per
     row the logits, the loss head, dy and dh = ReLU'(h) fp16(dy W2h) on MFMA without
@@ -372,7 +403,8 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
     gW1 / gb1 = dh^T [x | 1] with x generated from the records on chip (bgx_ppo_gw1:
     no feature rows in HBM).  Same fp16 operands, fp32 accumulation and per-row
     gradient scaling as _ppo_epoch_amp_manual; gradients land in p.grad as fp32.
-    The chunks' feature entries are not read."""
+    The chunks' feature entries are not read.  `guard` (a device bool, optional) is
+    set when the masked-action shortcut's bound (MASK_SHORTCUT_LIMIT) does not hold."""
     eps, c_v, c_e, gscale = coefs
     row_scale = gscale * n_total / min(n_total, REF_ROWS)
     post = min(n_total, REF_ROWS) / n_total
@@ -397,13 +429,15 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         w1pack = torch.empty(L.bgx_fc1_packed_size(Hd), dtype=torch.uint8, device=dev)
         check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
+        hmax2 = torch.zeros(1, dtype=torch.float32, device=dev) if guard is not None else None
         for _feats, _legal, actions, old_logp, returns, adv, records, *extra in chunks:
             prep = extra[0] if extra else {}
             rec = records.contiguous()
             m = rec.shape[0]
             perm, plan, row_plan = prep["plan"] if "plan" in prep else ppo_row_plan(rec, A)
             h = torch.empty(m, Hd, dtype=torch.float16, device=dev)
-            check(L.bgx_fc1_records(p(rec), m, p(w1pack), p(b1h), Hd, p(h), stream), "bgx_fc1_records")
+            check(L.bgx_fc1_records_ex(p(rec), m, p(w1pack), p(b1h), Hd, p(h), _ptr_or_none(hmax2), stream),
+                  "bgx_fc1_records_ex")
             dh = torch.empty(m, Hd, dtype=torch.float16, device=dev)
             stats = torch.empty(m, 4, dtype=torch.float32, device=dev)
             info = torch.empty(m, dtype=torch.int32, device=dev)
@@ -423,12 +457,16 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums):
         if post != 1.0:
             for t in (gW1, gW2, gb2):
                 t.mul_(post)
+        if guard is not None:
+            U = W2h[:A].float().norm(dim=1).max() * hmax2[0].sqrt() + b2h[:A].float().abs().max()
+            guard |= 2.0 * U > MASK_SHORTCUT_LIMIT
     W1.grad, b1.grad = gW1[:, :F_in].contiguous(), gW1[:, FEAT_BIAS_COL].contiguous()
     Wa.grad, ba.grad = gW2[:A].contiguous(), gb2[:A].contiguous()
     wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
 
 
-def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync=True):
+def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync=True, guard=None,
+                     fused_head=True):
     dev = next(net.parameters()).device
     if scaler.is_enabled():
         scaler.scale(torch.ones((), device=dev))          # initialises the scale tensor lazily
@@ -439,8 +477,8 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
     coefs = (EPS_CLIP, VALUE_LOSS_COEF, float(entropy_coef), float(scale) / n_total)
     manual = amp and _is_policy_mlp(net)
     if manual:
-        if _fused_head_ok(net):
-            _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums)
+        if fused_head and _fused_head_ok(net):
+            _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard)
         else:
             _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums)
         chunks = ()
@@ -479,6 +517,9 @@ class PPOTrainer:
         self.chunk = chunk
         self.fused = (self.dev.type == "cuda") if fused is None else fused
         self.amp = amp            # the reference's autocast (fp16 on the GPU); False = fp32 update
+        # the fused output layer + loss head (csrc/bg_ppo_fused.hip) while its exactness bound
+        # holds (MASK_SHORTCUT_LIMIT; update() falls back to the exact epoch otherwise)
+        self.fused_head = True
         # the B lanes as S engines on S streams (bench.py's C3 layout: one shard's policy
         # kernel runs beside the other's env step); shard 0 keeps the 1-shard seeds
         if shards is None:
@@ -654,10 +695,32 @@ class PPOTrainer:
         old = buf["logp"].reshape(-1)
         N = recs.shape[0]
 
-        # the fused path's features are encoded once and kept for the 4 epochs
-        # (fp16 under autocast: 2^21 rows x 198 x 2 B = 0.8 GB of HBM)
         manual = self.fused and self.amp and _is_policy_mlp(self.net)
-        fused_head = manual and _fused_head_ok(self.net)
+        fused_head = manual and _fused_head_ok(self.net) and self.fused_head
+        if not fused_head:
+            parts = self._epochs(recs, acts, old, R, adv, False)
+        else:
+            snap = self._snapshot()
+            guard = torch.zeros((), dtype=torch.bool, device=self.dev)
+            parts = self._epochs(recs, acts, old, R, adv, True, guard)
+            g = guard.to(torch.int32)
+            if _world(self.group) > 1:
+                dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.group)
+            if bool(g.item()):               # the masked-action shortcut's bound broke: redo exactly
+                print("[bgx] PPO update: logit bound above the fused head's exact range; update redone on the "
+                      "exact epoch, later updates too", flush=True)
+                self._restore(snap)
+                self.fused_head = False
+                parts = self._epochs(recs, acts, old, R, adv, False)
+        self.entropy_coef = entropy_coef_after_update(self.entropy_anneal, self.total_episodes)
+        p = (parts / NUM_EPOCHS).tolist()
+        return {"policy_loss": p[0], "value_loss": p[1], "entropy": p[2], "total_loss": p[3]}
+
+    def _epochs(self, recs, acts, old, R, adv, fused_head: bool, guard=None):
+        """The NUM_EPOCHS full-batch epochs of one update; returns the summed loss parts
+        (device, fp64)."""
+        N = recs.shape[0]
+        manual = self.fused and self.amp and _is_policy_mlp(self.net)
         # the fused head generates every feature it needs from the records (fc1 forward,
         # gW1); the other paths read features encoded once for the 4 epochs
         feats = [None if fused_head else
@@ -694,11 +757,43 @@ class PPOTrainer:
         parts = None
         for _ in range(NUM_EPOCHS):
             e = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
-                          amp=self.amp, fused=self.fused, sync=False)
+                          amp=self.amp, fused=self.fused, sync=False, guard=guard, fused_head=fused_head)
             parts = e if parts is None else parts + e
-        self.entropy_coef = entropy_coef_after_update(self.entropy_anneal, self.total_episodes)
-        p = (parts / NUM_EPOCHS).tolist()
-        return {"policy_loss": p[0], "value_loss": p[1], "entropy": p[2], "total_loss": p[3]}
+        return parts
+
+    def _snapshot_tensors(self):
+        ts = [p for p in self.net.parameters()]
+        for p in self.net.parameters():
+            ts += [v for _, v in sorted(self.opt.state[p].items()) if torch.is_tensor(v)] if p in self.opt.state else []
+        ts += [t for t in (getattr(self.scaler, "_scale", None), getattr(self.scaler, "_growth_tracker", None))
+               if torch.is_tensor(t)]
+        return ts
+
+    def _snapshot(self):
+        """The weights, the Adam state and the GradScaler state (no host sync) as one
+        concatenated device copy per dtype, so that an update can be redone."""
+        ts = self._snapshot_tensors()
+        flat = {}
+        for dt in {t.dtype for t in ts}:
+            flat[dt] = torch.cat([t.detach().reshape(-1) for t in ts if t.dtype == dt])
+        keys = {id(p) for p in self.net.parameters() if p in self.opt.state}
+        scal = {k: torch.is_tensor(getattr(self.scaler, k, None)) for k in ("_scale", "_growth_tracker")}
+        return flat, keys, scal
+
+    def _restore(self, snap):
+        flat, keys, scal = snap
+        with torch.no_grad():
+            for p in self.net.parameters():
+                if id(p) not in keys:                # no Adam state before the update: none after it
+                    self.opt.state.pop(p, None)
+            for k, had in scal.items():
+                if not had:
+                    setattr(self.scaler, k, None)    # lazily re-initialised, as before the update
+            off = {dt: 0 for dt in flat}
+            for t in self._snapshot_tensors():
+                n = t.numel()
+                t.copy_(flat[t.dtype][off[t.dtype]:off[t.dtype] + n].view_as(t))
+                off[t.dtype] += n
 
     def iteration(self):
         t0 = time.perf_counter()

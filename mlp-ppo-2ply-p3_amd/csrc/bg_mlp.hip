@@ -575,7 +575,7 @@ __global__ void k_fc1_pack(const _Float16* __restrict__ w1h, int hidden, int T, 
 template <int T>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_fc1_rec(const uint8_t* __restrict__ recs, int n,
                                                   const uint4* __restrict__ w1f, const _Float16* __restrict__ b1h,
-                                                  int hidden, _Float16* __restrict__ hout) {
+                                                  int hidden, _Float16* __restrict__ hout, float* __restrict__ hmax2) {
     // the W1 fragments live in LDS for the workgroup's lifetime (T = 4: 52 KiB, shared by
     // 8 waves; the bias is added in the epilogue from LDS, as the GEMM epilogue adds it, so
     // the kernel fits 128 VGPRs: 4 waves/SIMD); each wave walks 32-row tiles grid-strided, the next tile's records loaded behind the
@@ -591,6 +591,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     const int j = l & 31, h = l >> 5;
     const int ntiles = (n + 31) / 32, stride = gridDim.x * 8;
     int tile = blockIdx.x * 8 + wv;
+    __shared__ float swm[8];
+    float hm = 0.0f;
     const int r = l >> 1, off = (l & 1) * 32;
     uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
     if (tile < ntiles) {
@@ -629,6 +631,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(sw[(kb * T + t) * 64 + l]), bf, acc[t], 0, 0, 0);
         }
         __builtin_amdgcn_wave_barrier();                // srec reads done before the next tile's stores
+        float ss = 0.0f;                                // this lane's part of the row's |h|^2
         if (row0 + j < n) {
             _Float16* orow = hout + (size_t)(row0 + j) * hidden;
             #pragma unroll
@@ -640,10 +643,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
                         h4 v;
                         #pragma unroll
-                        for (int i = 0; i < 4; ++i) v[i] = (_Float16)fmaxf(acc[t][4 * q + i] + sb[u + i], 0.0f);
+                        for (int i = 0; i < 4; ++i) {
+                            v[i] = (_Float16)fmaxf(acc[t][4 * q + i] + sb[u + i], 0.0f);
+                            ss = fmaf((float)v[i], (float)v[i], ss);
+                        }
                         *(h4*)(orow + u) = v;
                     }
                 }
+        }
+        hm = fmaxf(hm, ss + __shfl_xor(ss, 32));        // this lane's row: both halves' parts
+    }
+    if (hmax2) {                                        // max |h_row|^2 of the workgroup, one atomic
+        #pragma unroll
+        for (int o = 16; o > 0; o >>= 1) hm = fmaxf(hm, __shfl_xor(hm, o));
+        if (l == 0) swm[wv] = hm;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float m = swm[0];
+            for (int w = 1; w < 8; ++w) m = fmaxf(m, swm[w]);
+            atomicMax((int*)hmax2, __float_as_int(m));      // non-negative: int order = float order
         }
     }
 }
@@ -749,6 +767,11 @@ int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* st
 
 int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_dev, const void* b1h_dev,
                     int32_t hidden, void* h_dev, void* stream) {
+    return bgx_fc1_records_ex(records_dev, n, packed_dev, b1h_dev, hidden, h_dev, nullptr, stream);
+}
+
+int bgx_fc1_records_ex(const uint8_t* records_dev, int32_t n, const void* packed_dev, const void* b1h_dev,
+                       int32_t hidden, void* h_dev, float* hmax2_dev, void* stream) {
     if (bgx_fc1_packed_size(hidden) < 0 || n < 0 || (n > 0 && (!records_dev || !packed_dev || !b1h_dev || !h_dev)))
         return BGX_EINVAL;
     if (((uintptr_t)records_dev | (uintptr_t)packed_dev) % 16 || (uintptr_t)h_dev % 8) return BGX_EINVAL;
@@ -761,10 +784,10 @@ int bgx_fc1_records(const uint8_t* records_dev, int32_t n, const void* packed_de
     const _Float16* b = (const _Float16*)b1h_dev;
     _Float16* o = (_Float16*)h_dev;
     switch (T) {
-        case 1: hipLaunchKernelGGL((k_fc1_rec<1>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
-        case 2: hipLaunchKernelGGL((k_fc1_rec<2>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
-        case 3: hipLaunchKernelGGL((k_fc1_rec<3>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
-        default: hipLaunchKernelGGL((k_fc1_rec<4>), grid, blk, 0, s, records_dev, n, w, b, hidden, o); break;
+        case 1: hipLaunchKernelGGL((k_fc1_rec<1>), grid, blk, 0, s, records_dev, n, w, b, hidden, o, hmax2_dev); break;
+        case 2: hipLaunchKernelGGL((k_fc1_rec<2>), grid, blk, 0, s, records_dev, n, w, b, hidden, o, hmax2_dev); break;
+        case 3: hipLaunchKernelGGL((k_fc1_rec<3>), grid, blk, 0, s, records_dev, n, w, b, hidden, o, hmax2_dev); break;
+        default: hipLaunchKernelGGL((k_fc1_rec<4>), grid, blk, 0, s, records_dev, n, w, b, hidden, o, hmax2_dev); break;
     }
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }

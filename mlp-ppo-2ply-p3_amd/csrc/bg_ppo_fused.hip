@@ -670,29 +670,34 @@ __global__ __launch_bounds__(448) void k_ppo_gw1(Gw1Args a) {
         for (int i = 0; i < 16; ++i) acc[u][i] = 0.0f;
     // loaders: dh = 512 16-byte chunks per tile (threads take chunk tid, and tid + 448
     // for tid < 64); records = 32 rows x 14 dwords (bytes 0..55), one per thread
+    // two tiles in flight: the loads of tile t + 2 are issued while tile t is computed
+    // (one tile ahead left the kernel waiting on HBM latency: 180 us per 2^20 rows)
     const uint4 z4 = make_uint4(0, 0, 0, 0);
-    uint4 d0 = z4, d1 = z4;
-    uint32_t rw = 0;
+    struct Ld { uint4 d0, d1; uint32_t rw; };
     const int rr = tid / 14, rwd = tid - 14 * (tid / 14);
     auto load = [&](int tile) {
+        Ld x{z4, z4, 0u};
+        if (tile >= t1) return x;
         const int row0 = tile * 32;
-        d0 = row0 + (tid >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (tid >> 4)) * kH))[tid & 15] : z4;
+        x.d0 = row0 + (tid >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (tid >> 4)) * kH))[tid & 15] : z4;
         if (tid < 64) {
             const int i = tid + 448;
-            d1 = row0 + (i >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (i >> 4)) * kH))[i & 15] : z4;
+            x.d1 = row0 + (i >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (i >> 4)) * kH))[i & 15] : z4;
         }
         const int gr = row0 + rr < a.m ? row0 + rr : a.m - 1;
-        rw = ((const uint32_t*)(a.rec + (size_t)gr * 64))[rwd];
+        x.rw = ((const uint32_t*)(a.rec + (size_t)gr * 64))[rwd];
+        return x;
     };
-    if (t0 < t1) load(t0);
+    Ld q0 = load(t0), q1 = load(t0 + 1);
     int buf = 0;
     for (int tile = t0; tile < t1; ++tile, buf ^= 1) {
-        *(uint4*)(sdh[buf] + swz(tid >> 4, tid & 15)) = d0;
-        if (tid < 64) *(uint4*)(sdh[buf] + swz((tid + 448) >> 4, (tid + 448) & 15)) = d1;
+        *(uint4*)(sdh[buf] + swz(tid >> 4, tid & 15)) = q0.d0;
+        if (tid < 64) *(uint4*)(sdh[buf] + swz((tid + 448) >> 4, (tid + 448) & 15)) = q0.d1;
         #pragma unroll
-        for (int q = 0; q < 4; ++q) srt[buf][(4 * rwd + q) * 32 + rr] = (uint8_t)(rw >> (8 * q));
+        for (int q = 0; q < 4; ++q) srt[buf][(4 * rwd + q) * 32 + rr] = (uint8_t)(q0.rw >> (8 * q));
         __syncthreads();
-        if (tile + 1 < t1) load(tile + 1);                 // next tile in flight behind the MFMAs
+        q0 = q1;
+        q1 = load(tile + 2);                                // behind this tile's MFMAs
         #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const uint8_t* bp = srt[buf] + byte * 32 + 16 * s + 4 * hh;
@@ -737,6 +742,23 @@ __global__ __launch_bounds__(256) void k_ppo_gw1_sum2(const float* __restrict__ 
     for (int g = 0; g < kRed; ++g) s += part2[(size_t)g * kGw1Part + e];
     const int f = e / kH, u = e - kH * f;
     gw1[u * kW1 + f] += s;
+}
+
+
+// ---- discounted returns per game lane (bgx.train.lane_returns; ppo_agent.py:206-216
+// restated per lane): R_t = r_t + gamma R_{t+1}, R reset at done -- one thread per lane
+// walking its T steps backwards, the same two fp32 roundings as the torch ops (no fma)
+__global__ __launch_bounds__(256) void k_lane_returns(const float* __restrict__ r, const uint8_t* __restrict__ d,
+                                                      int T, int B, float gamma, float* __restrict__ out) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    float R = 0.0f;
+    for (int t = T - 1; t >= 0; --t) {
+        const size_t i = (size_t)t * B + b;
+        if (d[i]) R = 0.0f;
+        R = __fadd_rn(r[i], __fmul_rn(gamma, R));
+        out[i] = R;
+    }
 }
 
 }  // namespace
@@ -824,6 +846,16 @@ extern "C" int bgx_ppo_gw1(const void* dh, const uint8_t* records, int32_t m, in
     float* part2 = workspace + (size_t)wgs * kGw1Part;
     hipLaunchKernelGGL(k_ppo_gw1_sum1, dim3((kGw1Part + 255) / 256, kRed), dim3(256), 0, s, workspace, wgs, part2);
     hipLaunchKernelGGL(k_ppo_gw1_sum2, dim3((kW1 * kH + 255) / 256), dim3(256), 0, s, part2, gw1);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
+extern "C" int bgx_lane_returns(const float* rewards, const uint8_t* dones, int32_t T, int32_t B, float gamma,
+                                float* out, void* stream) {
+    if (T < 0 || B < 0 || (T > 0 && B > 0 && (!rewards || !dones || !out))) return BGX_EINVAL;
+    if (T == 0 || B == 0) return BGX_OK;
+    hipLaunchKernelGGL(k_lane_returns, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream, rewards, dones, T, B,
+                       gamma, out);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }

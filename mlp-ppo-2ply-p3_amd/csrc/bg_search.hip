@@ -1224,7 +1224,7 @@ static int eval_waves(int NT) { return NT <= 4 ? kEvalNarrowWaves : kEvalWideWav
 // (k_eval_rw_*) except at NT = 4 (208 VGPRs of weights in one wave; LDS weights)
 struct EvalPick { EvalFn fn; int threads; };
 static EvalPick eval_kernel(int NT) {
-    if (const char* f = getenv("BGX_EVAL_FORM"); f && f[0] == 'l') {      // A/B: the LDS-weight form
+    if (const char* f = getenv("BGX_EVAL_FORM"); !(f && f[0] == 'r')) {   // default: the LDS-weight form (A/B "r")
         switch (NT) {
             case 1: return {k_eval<1>, 64 * eval_waves(1)}; case 2: return {k_eval<2>, 64 * eval_waves(2)};
             case 3: return {k_eval<3>, 64 * eval_waves(3)}; case 4: return {k_eval<4>, 64 * eval_waves(4)};

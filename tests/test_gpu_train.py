@@ -242,3 +242,48 @@ def test_rollout_graphs_match_eager():
     a = trs[0].buf["records"][:, :16384]
     b = trs[0].buf["records"][:, 16384:]
     assert not torch.equal(a, b)
+
+
+def test_fused_head_bound_guard_redoes_update():
+    """the fused head leaves a legal row's masked logits out of its
+    log-sum-exp, exact while 2U + log(1e-45) < -30 (U bounds |logit|).  With the
+    action head scaled up 60x the bound breaks: PPOTrainer must detect it, restore the
+    weights / Adam / GradScaler state and redo the update on the exact epoch -- the
+    result then equals a trainer that ran the exact epoch from the start."""
+    from bgx.train import PPOTrainer
+    trs = []
+    for fused_head in (True, False):
+        tr = PPOTrainer(batch=2048, horizon=4, seed=9, chunk=4096)
+        with torch.no_grad():
+            tr.net.action_head.weight.mul_(60.0)
+        tr.fused_head = fused_head
+        tr.rollout()
+        trs.append(tr)
+    # both trainers start from the same weights and rollout
+    for a, b in zip(trs[0].net.parameters(), trs[1].net.parameters()):
+        assert torch.equal(a, b)
+    assert torch.equal(trs[0].buf["actions"], trs[1].buf["actions"])
+    m0, m1 = trs[0].update(), trs[1].update()
+    assert trs[0].fused_head is False                     # the guard fired
+    for a, b in zip(trs[0].net.parameters(), trs[1].net.parameters()):
+        assert torch.equal(a, b)
+    assert m0 == m1
+    # and the reference-scale network keeps the fused head
+    tr = PPOTrainer(batch=2048, horizon=4, seed=9, chunk=4096)
+    tr.iteration()
+    assert tr.fused_head is True
+
+
+def test_lane_returns_kernel_matches_torch_loop():
+    """bgx_lane_returns (one thread per lane) == the torch per-step loop, bit for bit
+    (same two fp32 roundings, no fma), on a real rollout with game ends."""
+    from bgx.train import PPOTrainer, lane_returns, _lane_returns_torch
+    tr = PPOTrainer(batch=4096, horizon=16, seed=2)
+    tr.rollout()
+    r, d = tr.buf["rewards"], tr.buf["dones"]
+    assert int(d.sum()) > 0
+    assert torch.equal(lane_returns(r, d), _lane_returns_torch(r, d))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    r2 = torch.randn(33, 1000, device="cuda", generator=g)
+    d2 = (torch.rand(33, 1000, device="cuda", generator=g) < 0.1).to(torch.uint8)
+    assert torch.equal(lane_returns(r2, d2), _lane_returns_torch(r2, d2))

@@ -79,9 +79,9 @@ def window(steps, shift=False, tag=None):
         with torch.cuda.stream(streams[0]):
             row[0].replay()
         if shift and j == 0:
-            ev = torch.cuda.Event()
-            ev.record(streams[0])
-            streams[1].wait_event(ev)
+            sev = torch.cuda.Event()
+            sev.record(streams[0])
+            streams[1].wait_event(sev)
         with torch.cuda.stream(streams[1]):
             row[1].replay()
     t1 = time.perf_counter()
