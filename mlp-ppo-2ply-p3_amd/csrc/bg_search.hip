@@ -875,15 +875,117 @@ void k_eval(EvalArgs E) {
 //  * narrow (H <= 48): one wave holds every tile's fragments (13 x NT uint4; 156
 //    VGPRs at H = 40) and walks its own 32-leaf tiles; the head weights (epilogue
 //    only) stay in LDS.
+// Wide form, staged: a workgroup of NW waves takes sets of 128 pool leaves (4 leaf
+// tiles of 32 columns).  The pool entries and their row data reach LDS through a
+// software pipeline run by three loader roles (wave 0 keys, wave 1 tags, wave 2 the
+// dependent row side + max length), issued two and three sets ahead and stored one
+// iteration later, so no wave waits on HBM in the K loop; every wave then walks the
+// 4 leaf tiles one after the other (one 16-register accumulator live: 26 MFMAs per
+// tile, weights in registers, features from the unit table), writes its 32 units'
+// part of V, and after the next barrier wave n finishes leaf tile n.
+constexpr int kSetLeaves = 128, kSetTiles = 4;
+// ring slots: raw(k) lands at iteration k - 2 and is last read when set k is finished
+// (iteration k + 1, after that iteration's barrier, while a faster wave may already
+// land raw(k + 4)): 5 slots; row(k) lands at k - 1, the same last reader: 4 slots
+constexpr int kRawSlots = 5, kRowSlots = 4;
+struct StRaw { uint4 key[kSetLeaves]; uint32_t tag[kSetLeaves]; };
+struct StRow { uint4 side[kSetLeaves]; uint32_t ml[kSetLeaves]; };
+
+__device__ __forceinline__ Leaf leaf_from_lds(const StRaw& r, const StRow& w, int i) {
+    return make_leaf(LeafRaw{r.key[i], r.tag[i]}, LeafRow{w.side[i], w.ml[i]});
+}
+
+// The staging pipeline shared by the register-weight evaluators.  Step k of a
+// workgroup is pool set s0 + k G.  Loader roles: wave 0 the 128 keys, wave 1 the
+// 128 tags, wave 2 the row side + max length of each leaf (which needs the tag: it
+// reads it from LDS).  raw(k) is issued at iteration k - 3 and lands (LDS store) at
+// k - 2; row(k) is issued at k - 2 and lands at k - 1; set k is computed at
+// iteration k and finished at k + 1.
+struct Stager {
+    StRaw* sraw;
+    StRow* srow;
+    const EvalArgs* E;
+    long long s0, G, sets;
+    int wv, l;
+    uint4 ka, kb2;
+    uint32_t ta, tb, ma, mb;
+
+    __device__ bool live(int k) const { return s0 + (long long)k * G < sets; }
+    __device__ unsigned long long base(int k) const { return (unsigned long long)(s0 + (long long)k * G) * kSetLeaves; }
+    __device__ void load_raw(int k) {
+        if (!live(k)) return;
+        if (wv == 0) { ka = E->keys[base(k) + l]; kb2 = E->keys[base(k) + 64 + l]; }
+        else if (wv == 1) { ta = E->tags[base(k) + l]; tb = E->tags[base(k) + 64 + l]; }
+    }
+    __device__ void store_raw(int k) {
+        if (!live(k)) return;
+        StRaw& r = sraw[k % kRawSlots];
+        if (wv == 0) { r.key[l] = ka; r.key[64 + l] = kb2; }
+        else if (wv == 1) { r.tag[l] = ta; r.tag[64 + l] = tb; }
+    }
+    __device__ void load_row(int k) {
+        if (wv != 2 || !live(k)) return;
+        const StRaw& r = sraw[k % kRawSlots];
+        const uint32_t t0 = r.tag[l], t1 = r.tag[64 + l];
+        const int j0 = t0 != kTagNone ? (int)(t0 & 0x1FFFFFFFu) : 0, j1 = t1 != kTagNone ? (int)(t1 & 0x1FFFFFFFu) : 0;
+        ka = E->rowside[j0 / 21]; kb2 = E->rowside[j1 / 21];
+        ma = E->maxlen[j0]; mb = E->maxlen[j1];
+    }
+    __device__ void store_row(int k) {
+        if (wv != 2 || !live(k)) return;
+        StRow& w = srow[k % kRowSlots];
+        w.side[l] = ka; w.side[64 + l] = kb2; w.ml[l] = ma; w.ml[64 + l] = mb;
+    }
+    // raw(0), raw(1), row(0) in LDS; raw(2), row(1) in flight.  Ends with a barrier.
+    __device__ void prologue() {
+        load_raw(0); store_raw(0);
+        load_raw(1); store_raw(1);
+        __syncthreads();
+        if (wv == 2) { load_row(0); store_row(0); load_row(1); }
+        if (wv < 2) load_raw(2);
+    }
+    // iteration i: land raw(i + 2) / row(i + 1), barrier
+    __device__ void land(int i) {
+        if (wv < 2) store_raw(i + 2);
+        else store_row(i + 1);
+        __syncthreads();
+    }
+    // iteration i, after the barrier: issue raw(i + 3) / row(i + 2)
+    __device__ void issue(int i) {
+        if (wv < 2) load_raw(i + 3);
+        else load_row(i + 2);
+    }
+    __device__ const StRaw& raw(int k) const { return sraw[k % kRawSlots]; }
+    __device__ const StRow& row(int k) const { return srow[k % kRowSlots]; }
+};
+
+// the last step of the job-segmented min: leaf li of a finished set with value vv
+__device__ __forceinline__ void finish_leaf(const EvalArgs& E, const StRaw& r, const StRow& w, int li, int c, int h,
+                                            float vv) {
+    const uint32_t tag = r.tag[li];
+    const bool valid = tag != kTagNone && w.ml[li] == (tag >> 29);
+    const int jb = valid ? (int)(tag & 0x1FFFFFFFu) : -1;
+    if (!valid) vv = INFINITY;
+    #pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+        const float v2 = __shfl_down(vv, o, 32);
+        const int j2 = __shfl_down(jb, o, 32);
+        if (c + o < 32 && j2 == jb) vv = fminf(vv, v2);
+    }
+    const int jp = __shfl_up(jb, 1, 32);
+    if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
+}
+
 template <int NT>
-__global__ __launch_bounds__(64 * (slices(NT) / 2)) __attribute__((amdgpu_waves_per_eu(2)))
-void k_eval_rw_wide(EvalArgs E) {
+__global__ __launch_bounds__(64 * (slices(NT) / 2)) void k_eval_rw_wide(EvalArgs E) {
     static_assert(wide_tiles(NT), "wide form");
     constexpr int NW = slices(NT) / 2, NS = slices(NT);
-    __shared__ float part[2][NW][64];
+    static_assert(NW >= 3, "loader roles need 3 waves");
+    __shared__ StRaw sraw[kRawSlots];
+    __shared__ StRow srow[kRowSlots];
+    __shared__ float part[2][NW][kSetLeaves];
     __shared__ uint4 utab[256];
     build_unit_table(utab);
-    __syncthreads();
     const int l = lane_id(), h = l >> 5, c = l & 31, wv = threadIdx.x >> 6;
     uint4 wh[kKB], wl[kKB];
     #pragma unroll
@@ -895,88 +997,83 @@ void k_eval_rw_wide(EvalArgs E) {
     #pragma unroll
     for (int r4 = 0; r4 < 4; ++r4) hw[r4] = reinterpret_cast<const float4*>(E.wvq)[(wv * 4 + r4) * 64 + l];
     const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
-    const unsigned long long tiles = used / 64;
-    unsigned long long tile = *E.lo / 64 + blockIdx.x;
-    if (tile >= tiles) return;                      // the whole workgroup: same tiles for every wave
-    LeafRaw raw[2];
-    LeafRow row[2];
-    #pragma unroll
-    for (int n = 0; n < 2; ++n) { raw[n] = load_raw(E, tile * 64 + 32 * n + c); row[n] = load_row(E, raw[n]); }
-    int buf = 0;
-    for (; tile < tiles; tile += gridDim.x, buf ^= 1) {
-        Leaf L[2];
-        #pragma unroll
-        for (int n = 0; n < 2; ++n) L[n] = make_leaf(raw[n], row[n]);
-        const unsigned long long nxt = tile + gridDim.x < tiles ? tile + gridDim.x : tile;
-        #pragma unroll
-        for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
-        f32x16 x0, x1;
-        #pragma unroll
-        for (int kb = 0; kb < kKB; ++kb) {
-            const f16x8 f0 = feat16t(L[0], kb, h, utab), f1 = feat16t(L[1], kb, h, utab);
-            const f16x8 ah = __builtin_bit_cast(f16x8, wh[kb]), al = __builtin_bit_cast(f16x8, wl[kb]);
-            x0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, kb == 0 ? (f32x16){} : x0, 0, 0, 0);
-            x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f1, kb == 0 ? (f32x16){} : x1, 0, 0, 0);
-            x0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f0, x0, 0, 0, 0);
-            x1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f1, x1, 0, 0, 0);
-        }
-        #pragma unroll
-        for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
-        float a0 = 0.0f, a1 = 0.0f;
-        #pragma unroll
-        for (int r4 = 0; r4 < 4; ++r4) {
-            a0 = fmaf(relu_raw(x0[4 * r4 + 0]), hw[r4].x, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 0]), hw[r4].x, a1);
-            a0 = fmaf(relu_raw(x0[4 * r4 + 1]), hw[r4].y, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 1]), hw[r4].y, a1);
-            a0 = fmaf(relu_raw(x0[4 * r4 + 2]), hw[r4].z, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 2]), hw[r4].z, a1);
-            a0 = fmaf(relu_raw(x0[4 * r4 + 3]), hw[r4].w, a0); a1 = fmaf(relu_raw(x1[4 * r4 + 3]), hw[r4].w, a1);
-        }
-        a0 += __shfl_xor(a0, 32);
-        a1 += __shfl_xor(a1, 32);
-        if (h == 0) { part[buf][wv][c] = a0; part[buf][wv][32 + c] = a1; }
-        __syncthreads();
-        if (wv < 2) {                                // wave n finishes leaf tile n
-            float vv = part[buf][0][32 * wv + c];
+    Stager st{sraw, srow, &E, (long long)(*E.lo / kSetLeaves) + blockIdx.x, (long long)gridDim.x,
+              (long long)(used / kSetLeaves), wv, l, {}, {}, 0u, 0u, 0u, 0u};
+    st.prologue();
+    if (!st.live(0)) return;                          // the whole workgroup (uniform)
+    auto finish = [&](int k) {                        // set k's parts are complete: wave n -> leaf tile n
+        for (int n = wv; n < kSetTiles; n += NW) {
+            const int li = 32 * n + c;
+            float vv = part[k & 1][0][li];
             #pragma unroll
-            for (int t = 1; t < NW; ++t) vv += part[buf][t][32 * wv + c];
-            vv += E.bv;
-            const int jb = wv == 0 ? L[0].job : L[1].job;
-            if (!(wv == 0 ? L[0].valid : L[1].valid)) vv = INFINITY;
+            for (int t = 1; t < NW; ++t) vv += part[k & 1][t][li];
+            finish_leaf(E, st.raw(k), st.row(k), li, c, h, vv + E.bv);
+        }
+    };
+    int i = 0;
+    for (; st.live(i); ++i) {
+        st.land(i);
+        if (i > 0) finish(i - 1);
+        st.issue(i);
+        const StRaw& r = st.raw(i);
+        const StRow& w = st.row(i);
+        #pragma unroll 1
+        for (int n = 0; n < kSetTiles; ++n) {
+            const Leaf L = leaf_from_lds(r, w, 32 * n + c);
+            f32x16 x;
             #pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                const float v2 = __shfl_down(vv, o, 32);
-                const int j2 = __shfl_down(jb, o, 32);
-                if (c + o < 32 && j2 == jb) vv = fminf(vv, v2);
+            for (int kb = 0; kb < kKB; ++kb) {
+                const f16x8 f = feat16t(L, kb, h, utab);
+                x = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wh[kb]), f,
+                                                           kb == 0 ? (f32x16){} : x, 0, 0, 0);
+                x = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wl[kb]), f, x, 0, 0, 0);
             }
-            const int jp = __shfl_up(jb, 1, 32);
-            if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
+            float a = 0.0f;
+            #pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                a = fmaf(relu_raw(x[4 * r4 + 0]), hw[r4].x, a);
+                a = fmaf(relu_raw(x[4 * r4 + 1]), hw[r4].y, a);
+                a = fmaf(relu_raw(x[4 * r4 + 2]), hw[r4].z, a);
+                a = fmaf(relu_raw(x[4 * r4 + 3]), hw[r4].w, a);
+            }
+            a += __shfl_xor(a, 32);
+            if (h == 0) part[i & 1][wv][32 * n + c] = a;
         }
     }
+    __syncthreads();                                  // the last set's parts
+    finish(i - 1);
 }
 
+// Narrow form, staged (H <= 48): the same pipeline; a workgroup of 4 waves, wave n
+// holding every unit tile (13 x NT fragments, 156 VGPRs at H = 40) and computing
+// leaf tile n of each set start to end (no parts to exchange).
 template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_eval_rw_narrow(EvalArgs E) {
     static_assert(NT <= 3, "narrow register form: at most 3 tiles (156 VGPRs of weights)");
+    __shared__ StRaw sraw[kRawSlots];
+    __shared__ StRow srow[kRowSlots];
     __shared__ float wvs[NT * 8 * 64];
     __shared__ uint4 utab[256];
     for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = E.wvq[i];
     build_unit_table(utab);
-    __syncthreads();
-    const int l = lane_id(), h = l >> 5, c = l & 31;
+    const int l = lane_id(), h = l >> 5, c = l & 31, wv = threadIdx.x >> 6;
     uint4 wq[NT][kKB];
     #pragma unroll
     for (int t = 0; t < NT; ++t)
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) wq[t][kb] = E.w1q[(kb * NT + t) * 64 + l];
     const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
-    const unsigned long long tiles = used / 32;
-    const unsigned long long stride = (unsigned long long)gridDim.x * 4;
-    unsigned long long tile = *E.lo / 32 + (unsigned long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= tiles) return;
-    LeafRaw raw = load_raw(E, tile * 32 + c);
-    LeafRow row = load_row(E, raw);
-    for (; tile < tiles; tile += stride) {
-        const Leaf L = make_leaf(raw, row);
-        const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
+    Stager st{sraw, srow, &E, (long long)(*E.lo / kSetLeaves) + blockIdx.x, (long long)gridDim.x,
+              (long long)(used / kSetLeaves), wv, l, {}, {}, 0u, 0u, 0u, 0u};
+    st.prologue();                                    // (also orders wvs / utab)
+    if (!st.live(0)) return;
+    for (int i = 0; st.live(i); ++i) {
+        st.land(i);
+        st.issue(i);
+        const StRaw& r = st.raw(i);
+        const StRow& w = st.row(i);
+        const int li = 32 * wv + c;
+        const Leaf L = leaf_from_lds(r, w, li);
         f32x16 x[NT];
         #pragma unroll
         for (int kb = 0; kb < kKB; ++kb) {
@@ -985,9 +1082,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             for (int t = 0; t < NT; ++t)
                 x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wq[t][kb]), f,
                                                               kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
-            if (kb == 6) raw = load_raw(E, nxt * 32 + c);   // the next tile's entries, mid-loop (registers)
         }
-        row = load_row(E, raw);
         // hi + lo, relu, times the head weights: two units per packed-fp32 add / fma
         typedef float f32x2 __attribute__((ext_vector_type(2)));
         f32x2 v2 = {0.0f, 0.0f};
@@ -995,24 +1090,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         for (int t = 0; t < NT; ++t)
             #pragma unroll
             for (int j = 0; j < 8; j += 2) {
-                const int r = j < 4 ? j : j + 4;
-                f32x2 u = f32x2{x[t][r], x[t][r + 1]} + f32x2{x[t][r + 4], x[t][r + 5]};
+                const int rr = j < 4 ? j : j + 4;
+                f32x2 u = f32x2{x[t][rr], x[t][rr + 1]} + f32x2{x[t][rr + 4], x[t][rr + 5]};
                 u.x = fmaxf(u.x, 0.0f);
                 u.y = fmaxf(u.y, 0.0f);
                 v2 = __builtin_elementwise_fma(u, f32x2{wvs[(t * 8 + j) * 64 + l], wvs[(t * 8 + j + 1) * 64 + l]}, v2);
             }
         float v = v2.x + v2.y;
         v += __shfl_xor(v, 32) + E.bv;
-        const int jb = L.job;
-        float vv = L.valid ? v : INFINITY;
-        #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-            const float v2 = __shfl_down(vv, o, 32);
-            const int j2 = __shfl_down(jb, o, 32);
-            if (c + o < 32 && j2 == jb) vv = fminf(vv, v2);
-        }
-        const int jp = __shfl_up(jb, 1, 32);
-        if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
+        finish_leaf(E, r, w, li, c, h, v);
     }
 }
 
