@@ -279,8 +279,11 @@ def test_lane_returns_kernel_matches_torch_loop():
     (same two fp32 roundings, no fma), on a real rollout with game ends."""
     from bgx.train import PPOTrainer, lane_returns, _lane_returns_torch
     tr = PPOTrainer(batch=4096, horizon=16, seed=2)
-    tr.rollout()
-    r, d = tr.buf["rewards"], tr.buf["dones"]
+    for _ in range(12):                  # games last ~60 plies: roll on until some end in the window
+        tr.rollout()
+        r, d = tr.buf["rewards"], tr.buf["dones"]
+        if int(d.sum()) > 0:
+            break
     assert int(d.sum()) > 0
     assert torch.equal(lane_returns(r, d), _lane_returns_torch(r, d))
     g = torch.Generator(device="cuda").manual_seed(1)
