@@ -570,6 +570,8 @@ struct Leaf {
     uint32_t bar[2], off[2];
     int q, job;
     bool valid;
+    uint32_t hits;     // the root mover's blots the reply hit (bit p = point p)
+    int row;           // the leaf's row (its job's, 0 for an unused slot)
 };
 
 struct EvalArgs {
@@ -584,6 +586,8 @@ struct EvalArgs {
     const uint4* w1q;
     const float* wvq;
     float bv;
+    const float* rowpart;             // [rows][16 slices] the root mover's part of X1 per row (k_rowpart)
+    float* vdbg;                      // test hook (BGX_2PLY_DUMP): V per pool slot, else null
 };
 
 struct LeafRaw { uint4 key; uint32_t tag; };
@@ -606,7 +610,9 @@ __device__ __forceinline__ Leaf make_leaf(const LeafRaw& r, const LeafRow& w) {
     const bool used = r.tag != kTagNone;
     L.valid = used && w.ml == (r.tag >> 29);
     L.job = L.valid ? (int)(r.tag & 0x1FFFFFFFu) : -1;
+    L.row = used ? (int)(r.tag & 0x1FFFFFFFu) / 21 : 0;
     const uint32_t hits = key.w >> 8;
+    L.hits = L.valid ? hits : 0u;
     const uint64_t mlo = (((uint64_t)rs.y << 32) | rs.x) - spread4(hits & 0xFFFFu);
     const uint32_t mhi = rs.z - (uint32_t)spread4(hits >> 16);
     const uint32_t mbar = (rs.w & 15u) + (uint32_t)__builtin_popcount(hits), moff = (rs.w >> 4) & 15u;
@@ -656,10 +662,13 @@ __device__ __forceinline__ uint4 units_pair(uint32_t byte) {
 
 // the two point counts (nibbles) k-block kb < 12 takes from this lane's half h:
 // points 4 k6 + 2h, +1 = byte (2 k6 + h) of the player's 96-bit nibble vector
+__device__ __forceinline__ uint32_t side_byte(uint64_t lo, uint32_t hi, int k6, int h) {
+    const uint32_t dw = k6 < 2 ? (uint32_t)lo : (k6 < 4 ? (uint32_t)(lo >> 32) : hi);
+    return (dw >> (16 * (k6 & 1) + 8 * h)) & 0xFFu;
+}
 __device__ __forceinline__ uint32_t kb_byte(const Leaf& L, int kb, int h) {
     const int P = kb / 6, k6 = kb % 6;
-    const uint32_t dw = k6 < 2 ? (uint32_t)L.lo[P] : (k6 < 4 ? (uint32_t)(L.lo[P] >> 32) : L.hi[P]);
-    return (dw >> (16 * (k6 & 1) + 8 * h)) & 0xFFu;
+    return side_byte(L.lo[P], L.hi[P], k6, h);
 }
 
 // B operand of k-block kb for this lane's half h (permuted K order, kperm)
@@ -675,19 +684,6 @@ __device__ __forceinline__ f16x8 feat16(const Leaf& L, int kb, int h) {
         v = make_uint4(0u, 0u, 0u, 0u);
     }
     return __builtin_bit_cast(f16x8, v);
-}
-
-// feat16 with the point units read from a 256-entry LDS table instead of computed:
-// utab[b] = units_pair(b), the B-operand half-block of a point pair whose counts are
-// the two nibbles of byte b.  One ds_read_b128 replaces ~10 VALU per k-block and leaf
-// tile (the register-weight evaluators are otherwise VALU-issue-bound: 9 VALU per MFMA
-// at H = 40).
-__device__ __forceinline__ void build_unit_table(uint4* utab) {
-    for (int b = threadIdx.x; b < 256; b += blockDim.x) utab[b] = units_pair((uint32_t)b);
-}
-__device__ __forceinline__ f16x8 feat16t(const Leaf& L, int kb, int h, const uint4* utab) {
-    if (kb < 12) return __builtin_bit_cast(f16x8, utab[kb_byte(L, kb, h)]);
-    return feat16(L, kb, h);
 }
 
 __device__ __forceinline__ int ord_f32(float v) {
@@ -710,42 +706,50 @@ __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0
 // asm would hide the MFMA-result read from the hazard recognizer, which must pad it)
 __device__ __forceinline__ float relu_raw(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
+// Wide tiles (H > 64), one leaf tile of 32 columns at a time.  Two leaf tiles in flight
+// (sharing each weight fragment, 128 accumulator VGPRs at H = 128) gave wrong values in
+// columns 16-31 of the second tile for 0.01-0.8 % of leaves, varying with the build's
+// instruction layout; one tile at a time was exact on every leaf of every build tried
+// (test_two_ply_every_leaf_vs_fp64: all 534 k leaves of a 48-root batch against fp64).
 template <int NT>
-__device__ __forceinline__ void eval_leaves_wide(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z,
-                                                 float bias, float (&v)[2]) {
+__device__ __forceinline__ float eval_tile_wide(const uint4* wq, const float* wvs, const Leaf& L, int z, float bias) {
     constexpr int NW = slices(NT) / 2;
     const int l = lane_id(), h = l >> 5;
-    f32x16 x[2][NW];
+    f32x16 x[NW];
     #pragma unroll
     for (int kb = 0; kb < kKB; ++kb) {
-        const f16x8 f0 = feat16(L[0], kb, h), f1 = feat16(L[1], kb, h);
+        const f16x8 f = feat16(L, kb, h);
         #pragma unroll
         for (int t = 0; t < NW; ++t) {
             const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 0) * 64 + l + z]);
             const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 1) * 64 + l + z]);
-            x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f0, kb == 0 ? (f32x16){} : x[0][t], 0, 0, 0);
-            x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f1, kb == 0 ? (f32x16){} : x[1][t], 0, 0, 0);
-            x[0][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f0, x[0][t], 0, 0, 0);
-            x[1][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f1, x[1][t], 0, 0, 0);
+            x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+            x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f, x[t], 0, 0, 0);
         }
     }
     // value head: relu times the head weights, 4 registers' weights per ds_read_b128
-    float a[2] = {0.0f, 0.0f};
+    float a = 0.0f;
     #pragma unroll
     for (int t = 0; t < NW; ++t)
         #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4) {
             const float4 w = reinterpret_cast<const float4*>(wvs)[(t * 4 + r4) * 64 + l + z];
-            #pragma unroll
-            for (int n = 0; n < 2; ++n) {
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 0]), w.x, a[n]);
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 1]), w.y, a[n]);
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 2]), w.z, a[n]);
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 3]), w.w, a[n]);
-            }
+            a = fmaf(relu_raw(x[t][4 * r4 + 0]), w.x, a);
+            a = fmaf(relu_raw(x[t][4 * r4 + 1]), w.y, a);
+            a = fmaf(relu_raw(x[t][4 * r4 + 2]), w.z, a);
+            a = fmaf(relu_raw(x[t][4 * r4 + 3]), w.w, a);
         }
-    #pragma unroll
-    for (int n = 0; n < 2; ++n) v[n] = a[n] + __shfl_xor(a[n], 32) + bias;
+    return a + __shfl_xor(a, 32) + bias;
+}
+
+template <int NT>
+__device__ __forceinline__ void eval_leaves_wide(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z,
+                                                 float bias, float (&v)[2]) {
+    v[0] = eval_tile_wide<NT>(wq, wvs, L[0], z, bias);
+    __builtin_amdgcn_sched_barrier(0);              // the tiles stay apart (not interleaved)
+    int z1 = z;                                     // opaque: the second tile re-reads its fragments
+    __asm__ volatile("" : "+s"(z1));
+    v[1] = eval_tile_wide<NT>(wq, wvs, L[1], z1, bias);
 }
 
 template <int NT>
@@ -793,6 +797,252 @@ __device__ __forceinline__ void eval_leaves(const uint4* wq, const float* wvs, c
     for (int n = 0; n < 2; ++n) v[n] += __shfl_xor(v[n], 32) + bias;
 }
 
+// ---- round 4: the evaluator factored by row ----
+// X1 = W1s . f is linear in f, and a leaf's features are the replier's points (from
+// its key), block 12 (bars, offs, one-hot, bias) and the ROOT MOVER's points -- which
+// are the same for every leaf of a row (root, move a) except at the mover's blots the
+// reply hit (count 1 -> 0: u0 goes from 1 to 0, the other three units stay 0).  So
+// k_rowpart computes the mover's part of X1 once per row (its 6 point k-blocks, hi +
+// lo, fp32 accumulation) and a leaf pair starts its accumulators from it (C = rowpart
+// of each column's row), then runs the replier's 6 point k-blocks, block 12, and --
+// only for the mover k-blocks that hold a hit point of some leaf of the pair -- that
+// block's weights against the hit delta (-1 at u0 of each hit point): 7 + (hit
+// blocks) of the 13 k-blocks.  Which blocks are the replier's depends on q, so the
+// pair's valid leaves must share q (rows are laid out grouped by replier, k_scan);
+// a pair that mixes them takes the full 13-block form (eval_leaves).
+__device__ __forceinline__ f16x8 hit_delta(uint32_t hits, int k6, int h) {
+    const uint32_t b = (hits >> (4 * k6 + 2 * h)) & 3u;      // points 4 k6 + 2h, +1: elements 0, 1 (u0)
+    return __builtin_bit_cast(f16x8, make_uint4((b & 1u ? 0xBC00u : 0u) | (b & 2u ? 0xBC000000u : 0u), 0u, 0u, 0u));
+}
+
+// mask of the mover k-blocks (4 points each) that hold a hit point of any lane, wave-uniform
+__device__ __forceinline__ uint32_t hit_blocks(uint32_t hits) {
+    uint32_t m = 0u;
+    #pragma unroll
+    for (int k6 = 0; k6 < 6; ++k6) m |= __ballot((hits >> (4 * k6)) & 15u) ? 1u << k6 : 0u;
+    return m;
+}
+
+// what the factored form needs of a leaf: the replier's nibbles, the block-12 operand,
+// the hit mask and the row
+struct FLeaf {
+    uint64_t rlo;
+    uint32_t rhi;
+    uint32_t b12;      // bar0 | off0 << 8 | bar1 << 16 | off1 << 24 | q << 31
+    uint32_t hits;
+    int row;
+};
+__device__ __forceinline__ FLeaf fleaf(const Leaf& L) {
+    FLeaf F;
+    F.rlo = L.q ? L.lo[1] : L.lo[0];
+    F.rhi = L.q ? L.hi[1] : L.hi[0];
+    F.b12 = L.bar[0] | (L.off[0] << 8) | (L.bar[1] << 16) | (L.off[1] << 24) | ((uint32_t)L.q << 31);
+    F.hits = L.hits;
+    F.row = L.row;
+    return F;
+}
+// feat16(L, 12, h) from the packed form
+__device__ __forceinline__ f16x8 feat12(uint32_t b, int h) {
+    const uint32_t p1 = (b & 0xFFu) | ((b & 0xFF00u) << 8), p2 = ((b >> 16) & 0xFFu) | ((b >> 8) & 0x0F0000u);
+    const uint4 v = make_uint4(f16_pair(p1, 0.5f, 1.0f), f16_pair(p2, 0.5f, 1.0f), b >> 31 ? 0x3C00u : 0x3C000000u,
+                               0x3C00u);
+    return __builtin_bit_cast(f16x8, h ? make_uint4(0u, 0u, 0u, 0u) : v);
+}
+
+template <int NT, int NN>
+__device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* wvs, const FLeaf* L, int z,
+                                                 float bias, const float* rowpart, int q, float* v) {
+    constexpr bool kWide = wide_tiles(NT);
+    constexpr int NA = kWide ? slices(NT) / 2 : NT;      // accumulator tiles per 32 leaves
+    constexpr int HP = 16 * slices(NT);                  // rowpart row stride (floats)
+    const int l = lane_id(), h = l >> 5;
+    f32x16 x[NN][NA];
+    // narrow: the row parts are loaded first and added after the MFMAs (their latency hidden
+    // behind them; 15.9 vs 31.5 ms per C4 batch at H = 40); wide: they start the accumulators
+    // (30.6 vs 31.4 ms at H = 128)
+    constexpr bool kLate = !kWide;
+    float4 rpv[NN][NA][kWide ? 4 : 2];
+    if constexpr (kLate) {
+    #pragma unroll
+    for (int n = 0; n < NN; ++n) {
+        const float4* rp = reinterpret_cast<const float4*>(rowpart + (size_t)L[n].row * HP + 4 * h);
+        #pragma unroll
+        for (int t = 0; t < NA; ++t)
+            #pragma unroll
+            for (int j = 0; j < (kWide ? 4 : 2); ++j) rpv[n][t][j] = rp[(kWide ? 32 * t + 8 * j : 16 * t + 8 * j) / 4];
+    }
+    } else {
+    #pragma unroll
+    for (int n = 0; n < NN; ++n) {
+        const float4* rp = reinterpret_cast<const float4*>(rowpart + (size_t)L[n].row * HP + 4 * h);
+        #pragma unroll
+        for (int t = 0; t < NA; ++t) {
+            if constexpr (kWide) {           // register 4j + i <- unit 32t + 8j + 4h + i
+                #pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float4 a = rp[(32 * t + 8 * j) / 4];
+                    x[n][t][4 * j + 0] = a.x; x[n][t][4 * j + 1] = a.y;
+                    x[n][t][4 * j + 2] = a.z; x[n][t][4 * j + 3] = a.w;
+                }
+            } else {                         // hi rows: r 0-3 <- unit 16t + 4h + r, r 8-11 <- 16t + 8 + 4h + r - 8
+                const float4 a = rp[(16 * t) / 4], b = rp[(16 * t + 8) / 4];
+                x[n][t] = (f32x16){a.x, a.y, a.z, a.w, 0.0f, 0.0f, 0.0f, 0.0f, b.x, b.y, b.z, b.w, 0.0f, 0.0f, 0.0f, 0.0f};
+            }
+        }
+    }
+    }
+    auto block = [&](int kb, const f16x8 (&f)[NN], bool first) {
+        #pragma unroll
+        for (int t = 0; t < NA; ++t) {
+            if constexpr (kWide) {
+                const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * NA + t) * 2 + 0) * 64 + l + z]);
+                const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * NA + t) * 2 + 1) * 64 + l + z]);
+                #pragma unroll
+                for (int n = 0; n < NN; ++n) {
+                    x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f[n], first ? (f32x16){} : x[n][t], 0, 0, 0);
+                    x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f[n], x[n][t], 0, 0, 0);
+                }
+            } else {
+                const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + t) * 64 + l + z]);
+                #pragma unroll
+                for (int n = 0; n < NN; ++n)
+                    x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f[n], first ? (f32x16){} : x[n][t], 0, 0, 0);
+            }
+        }
+    };
+    // the replier's points (each column's own replier: a column of the other replier in
+    // this pass is discarded by the caller), then block 12
+    #pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        f16x8 f[NN];
+        #pragma unroll
+        for (int n = 0; n < NN; ++n) f[n] = __builtin_bit_cast(f16x8, units_pair(side_byte(L[n].rlo, L[n].rhi, j, h)));
+        block(6 * q + j, f, kLate && j == 0);
+    }
+    {
+        f16x8 f[NN];
+        #pragma unroll
+        for (int n = 0; n < NN; ++n) f[n] = feat12(L[n].b12, h);
+        block(12, f, false);
+    }
+    // the hit deltas, per mover k-block that holds a hit point of the leaves (wave-uniform test)
+    const int P = 1 - q;
+    uint32_t hall = 0u;
+    #pragma unroll
+    for (int n = 0; n < NN; ++n) hall |= L[n].hits;
+    #pragma unroll 1
+    for (uint32_t hb = hit_blocks(hall); hb; hb &= hb - 1u) {
+        const int k6 = __builtin_ctz(hb);
+        f16x8 f[NN];
+        #pragma unroll
+        for (int n = 0; n < NN; ++n) f[n] = hit_delta(L[n].hits, k6, h);
+        block(6 * P + k6, f, false);
+    }
+    if constexpr (kLate)
+    #pragma unroll
+    for (int n = 0; n < NN; ++n)
+        #pragma unroll
+        for (int t = 0; t < NA; ++t)
+            #pragma unroll
+            for (int j = 0; j < (kWide ? 4 : 2); ++j) {
+                const int r0 = kWide ? 4 * j : 8 * j;     // wide: regs 4j..; narrow: hi regs 0-3, 8-11
+                x[n][t][r0 + 0] += rpv[n][t][j].x; x[n][t][r0 + 1] += rpv[n][t][j].y;
+                x[n][t][r0 + 2] += rpv[n][t][j].z; x[n][t][r0 + 3] += rpv[n][t][j].w;
+            }
+    if constexpr (kWide) {
+        float a[NN];
+        #pragma unroll
+        for (int n = 0; n < NN; ++n) a[n] = 0.0f;
+        #pragma unroll
+        for (int t = 0; t < NA; ++t)
+            #pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const float4 w = reinterpret_cast<const float4*>(wvs)[(t * 4 + r4) * 64 + l + z];
+                #pragma unroll
+                for (int n = 0; n < NN; ++n) {
+                    a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 0]), w.x, a[n]);
+                    a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 1]), w.y, a[n]);
+                    a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 2]), w.z, a[n]);
+                    a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 3]), w.w, a[n]);
+                }
+            }
+        #pragma unroll
+        for (int n = 0; n < NN; ++n) v[n] = a[n] + __shfl_xor(a[n], 32) + bias;
+    } else {
+        #pragma unroll
+        for (int n = 0; n < NN; ++n) v[n] = 0.0f;
+        #pragma unroll
+        for (int n = 0; n < NN; ++n)
+            #pragma unroll
+            for (int t = 0; t < NT; ++t)
+                #pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int r = j < 4 ? j : j + 4;
+                    v[n] = fmaf(fmaxf(x[n][t][r] + x[n][t][r + 4], 0.0f), wvs[(t * 8 + j) * 64 + l + z], v[n]);
+                }
+        #pragma unroll
+        for (int n = 0; n < NN; ++n) v[n] += __shfl_xor(v[n], 32) + bias;
+    }
+}
+
+// rowpart[row][u] = sum over the root mover's 12 x 4 point features of (W1s hi + lo)[u]
+// x feature, fp32 accumulation, for every row (the mover's side of a from rowside, no
+// hits; the replier's side zero, so all 12 point k-blocks can run whatever the mover).
+// Units in the evaluators' accumulator order: narrow unit 16t + (r & 3) + 4h + 8(r >> 3)
+// is hi register r + lo register r + 4 of tile t; wide unit 32t + 8(r >> 2) + 4h + (r & 3).
+template <int NT>
+__global__ __launch_bounds__(256) void k_rowpart(const uint4* rowside, const int64_t* nrows, const uint4* w1q,
+                                                 float* rowpart) {
+    constexpr bool kWide = wide_tiles(NT);
+    constexpr int NA = kWide ? slices(NT) / 2 : NT, HP = 16 * slices(NT);
+    const int l = lane_id(), h = l >> 5, c = l & 31;
+    const long long rows = *nrows;
+    const long long tiles = (rows + 31) / 32;
+    for (long long tile = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); tile < tiles;
+         tile += (long long)gridDim.x * 4) {
+        const long long r = tile * 32 + c;
+        const bool in = r < rows;
+        const uint4 rs = in ? rowside[r] : make_uint4(0u, 0u, 0u, 0u);
+        const int P = 1 - (int)((rs.w >> 8) & 1u);
+        Leaf L{};
+        L.lo[P] = ((uint64_t)rs.y << 32) | rs.x;
+        L.hi[P] = rs.z;
+        f32x16 x[NA];
+        #pragma unroll
+        for (int kb = 0; kb < 12; ++kb) {
+            const f16x8 f = __builtin_bit_cast(f16x8, units_pair(kb_byte(L, kb, h)));
+            #pragma unroll
+            for (int t = 0; t < NA; ++t) {
+                if constexpr (kWide) {
+                    const f16x8 ah = __builtin_bit_cast(f16x8, w1q[((kb * NA + t) * 2 + 0) * 64 + l]);
+                    const f16x8 al = __builtin_bit_cast(f16x8, w1q[((kb * NA + t) * 2 + 1) * 64 + l]);
+                    x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+                    x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f, x[t], 0, 0, 0);
+                } else {
+                    const f16x8 a = __builtin_bit_cast(f16x8, w1q[(kb * NT + t) * 64 + l]);
+                    x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+                }
+            }
+        }
+        if (!in) continue;
+        float* out = rowpart + (size_t)r * HP + 4 * h;
+        #pragma unroll
+        for (int t = 0; t < NA; ++t) {
+            if constexpr (kWide) {
+                #pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    *reinterpret_cast<float4*>(out + 32 * t + 8 * j) =
+                        make_float4(x[t][4 * j], x[t][4 * j + 1], x[t][4 * j + 2], x[t][4 * j + 3]);
+            } else {
+                *reinterpret_cast<float4*>(out + 16 * t) =
+                    make_float4(x[t][0] + x[t][4], x[t][1] + x[t][5], x[t][2] + x[t][6], x[t][3] + x[t][7]);
+                *reinterpret_cast<float4*>(out + 16 * t + 8) =
+                    make_float4(x[t][8] + x[t][12], x[t][9] + x[t][13], x[t][10] + x[t][14], x[t][11] + x[t][15]);
+            }
+        }
+    }
+}
+
 // workgroup shape of the evaluators: 4 waves (NT <= 4: <= 52 KiB of weights in LDS,
 // several workgroups per CU) or 8 waves (H = 128: 120 KiB, one workgroup per CU,
 // two waves per SIMD)
@@ -813,7 +1063,7 @@ __device__ __forceinline__ void stage_weights(uint4* wq, float* wvs, const uint4
 // wave walks its own tiles with the next tile's pool entries in flight during the
 // current tile's MFMAs.
 template <int NT>
-__global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) __attribute__((amdgpu_waves_per_eu(NT <= 4 ? 3 : 2)))
+__global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) __attribute__((amdgpu_waves_per_eu(2)))
 void k_eval(EvalArgs E) {
     constexpr int W = EvalShape<NT>::kWaves;
     __shared__ uint4 wq[kKB * slices(NT) * 64];
@@ -839,9 +1089,41 @@ void k_eval(EvalArgs E) {
         #pragma unroll
         for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
         float v[2];
-        eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
+        if (E.rowpart) {
+            // the factored form once per replier among the pair's valid leaves (wave-uniform;
+            // rows grouped by replier make two rare), so a leaf's V never depends on its pair
+            const uint64_t b1 = __ballot((L[0].valid && L[0].q) || (L[1].valid && L[1].q));
+            const uint64_t b0 = __ballot((L[0].valid && !L[0].q) || (L[1].valid && !L[1].q));
+            v[0] = v[1] = 0.0f;
+            const FLeaf F[2] = {fleaf(L[0]), fleaf(L[1])};
+            #pragma unroll 1
+            for (int qq = b0 ? 0 : 1; qq <= (b1 ? 1 : 0); ++qq) {
+                float w[2];
+                int zq = z;                               // opaque per pass: no LDS read hoisted out
+                __asm__ volatile("" : "+s"(zq));
+                if constexpr (wide_tiles(NT)) {         // one leaf tile at a time (eval_tile_wide)
+                    eval_leaves_fact<NT, 1>(wq, wvs, &F[0], zq, E.bv, E.rowpart, qq, &w[0]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    int zr = zq;
+                    __asm__ volatile("" : "+s"(zr));
+                    eval_leaves_fact<NT, 1>(wq, wvs, &F[1], zr, E.bv, E.rowpart, qq, &w[1]);
+                } else {
+                    eval_leaves_fact<NT, 2>(wq, wvs, F, zq, E.bv, E.rowpart, qq, w);
+                }
+                #pragma unroll
+                for (int n = 0; n < 2; ++n) v[n] = L[n].q == qq ? w[n] : v[n];
+            }
+        } else {
+            eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
+        }
         #pragma unroll
-        for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
+        for (int n = 0; n < 2; ++n) {
+            row[n] = load_row(E, raw[n]);
+        }
+        if (E.vdbg && h == 0) {
+            E.vdbg[tile * 64 + c] = v[0];
+            E.vdbg[tile * 64 + 32 + c] = v[1];
+        }
         #pragma unroll
         for (int n = 0; n < 2; ++n) {
             const int jb = L[n].job;
@@ -856,249 +1138,6 @@ void k_eval(EvalArgs E) {
             const int jp = __shfl_up(jb, 1, 32);
             if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
         }
-    }
-}
-
-// ---- round 4: the evaluator with W1 resident in registers ----
-// k_eval above reads every W1 fragment from LDS just before the MFMA that uses it
-// (2 waves/SIMD at H = 128: no registers to prefetch a k-block ahead), so most MFMAs
-// wait on an LDS read (60 % MFMA busy).  Here no weight is loaded in the K loop:
-//  * wide (H > 64): a workgroup of NW = slices/2 waves, wave T holding unit tile T's
-//    hi and lo fragments for all 13 k-blocks (104 VGPRs) and its 32 head weights.
-//    The waves take the SAME 64 leaves (2 x 32 columns) per iteration, each
-//    generating their features in registers (7 VALU per k-block and leaf tile,
-//    hidden in the gaps of its 2 MFMAs) -- so no LDS traffic in the K loop at all --
-//    and each forms its 32 units' part of V; the parts meet in LDS (fixed order
-//    T = 0..NW-1, then + bias) and waves 0 and 1 finish one leaf tile each
-//    (segmented min, atomicMin per job).  One barrier per iteration (the part
-//    array is double-buffered).
-//  * narrow (H <= 48): one wave holds every tile's fragments (13 x NT uint4; 156
-//    VGPRs at H = 40) and walks its own 32-leaf tiles; the head weights (epilogue
-//    only) stay in LDS.
-// Wide form, staged: a workgroup of NW waves takes sets of 128 pool leaves (4 leaf
-// tiles of 32 columns).  The pool entries and their row data reach LDS through a
-// software pipeline run by three loader roles (wave 0 keys, wave 1 tags, wave 2 the
-// dependent row side + max length), issued two and three sets ahead and stored one
-// iteration later, so no wave waits on HBM in the K loop; every wave then walks the
-// 4 leaf tiles one after the other (one 16-register accumulator live: 26 MFMAs per
-// tile, weights in registers, features from the unit table), writes its 32 units'
-// part of V, and after the next barrier wave n finishes leaf tile n.
-constexpr int kSetLeaves = 128, kSetTiles = 4;
-// ring slots: raw(k) lands at iteration k - 2 and is last read when set k is finished
-// (iteration k + 1, after that iteration's barrier, while a faster wave may already
-// land raw(k + 4)): 5 slots; row(k) lands at k - 1, the same last reader: 4 slots
-constexpr int kRawSlots = 5, kRowSlots = 4;
-struct StRaw { uint4 key[kSetLeaves]; uint32_t tag[kSetLeaves]; };
-struct StRow { uint4 side[kSetLeaves]; uint32_t ml[kSetLeaves]; };
-
-__device__ __forceinline__ Leaf leaf_from_lds(const StRaw& r, const StRow& w, int i) {
-    return make_leaf(LeafRaw{r.key[i], r.tag[i]}, LeafRow{w.side[i], w.ml[i]});
-}
-
-// The staging pipeline shared by the register-weight evaluators.  Step k of a
-// workgroup is pool set s0 + k G.  Loader roles: wave 0 the 128 keys, wave 1 the
-// 128 tags, wave 2 the row side + max length of each leaf (which needs the tag: it
-// reads it from LDS).  raw(k) is issued at iteration k - 3 and lands (LDS store) at
-// k - 2; row(k) is issued at k - 2 and lands at k - 1; set k is computed at
-// iteration k and finished at k + 1.
-struct Stager {
-    StRaw* sraw;
-    StRow* srow;
-    const EvalArgs* E;
-    long long s0, G, sets;
-    int wv, l;
-    uint4 ka, kb2;
-    uint32_t ta, tb, ma, mb;
-
-    __device__ bool live(int k) const { return s0 + (long long)k * G < sets; }
-    __device__ unsigned long long base(int k) const { return (unsigned long long)(s0 + (long long)k * G) * kSetLeaves; }
-    __device__ void load_raw(int k) {
-        if (!live(k)) return;
-        if (wv == 0) { ka = E->keys[base(k) + l]; kb2 = E->keys[base(k) + 64 + l]; }
-        else if (wv == 1) { ta = E->tags[base(k) + l]; tb = E->tags[base(k) + 64 + l]; }
-    }
-    __device__ void store_raw(int k) {
-        if (!live(k)) return;
-        StRaw& r = sraw[k % kRawSlots];
-        if (wv == 0) { r.key[l] = ka; r.key[64 + l] = kb2; }
-        else if (wv == 1) { r.tag[l] = ta; r.tag[64 + l] = tb; }
-    }
-    __device__ void load_row(int k) {
-        if (wv != 2 || !live(k)) return;
-        const StRaw& r = sraw[k % kRawSlots];
-        const uint32_t t0 = r.tag[l], t1 = r.tag[64 + l];
-        const int j0 = t0 != kTagNone ? (int)(t0 & 0x1FFFFFFFu) : 0, j1 = t1 != kTagNone ? (int)(t1 & 0x1FFFFFFFu) : 0;
-        ka = E->rowside[j0 / 21]; kb2 = E->rowside[j1 / 21];
-        ma = E->maxlen[j0]; mb = E->maxlen[j1];
-    }
-    __device__ void store_row(int k) {
-        if (wv != 2 || !live(k)) return;
-        StRow& w = srow[k % kRowSlots];
-        w.side[l] = ka; w.side[64 + l] = kb2; w.ml[l] = ma; w.ml[64 + l] = mb;
-    }
-    // raw(0), raw(1), row(0) in LDS; raw(2), row(1) in flight.  Ends with a barrier.
-    __device__ void prologue() {
-        load_raw(0); store_raw(0);
-        load_raw(1); store_raw(1);
-        __syncthreads();
-        if (wv == 2) { load_row(0); store_row(0); load_row(1); }
-        if (wv < 2) load_raw(2);
-    }
-    // iteration i: land raw(i + 2) / row(i + 1), barrier
-    __device__ void land(int i) {
-        if (wv < 2) store_raw(i + 2);
-        else store_row(i + 1);
-        __syncthreads();
-    }
-    // iteration i, after the barrier: issue raw(i + 3) / row(i + 2)
-    __device__ void issue(int i) {
-        if (wv < 2) load_raw(i + 3);
-        else load_row(i + 2);
-    }
-    __device__ const StRaw& raw(int k) const { return sraw[k % kRawSlots]; }
-    __device__ const StRow& row(int k) const { return srow[k % kRowSlots]; }
-};
-
-// the last step of the job-segmented min: leaf li of a finished set with value vv
-__device__ __forceinline__ void finish_leaf(const EvalArgs& E, const StRaw& r, const StRow& w, int li, int c, int h,
-                                            float vv) {
-    const uint32_t tag = r.tag[li];
-    const bool valid = tag != kTagNone && w.ml[li] == (tag >> 29);
-    const int jb = valid ? (int)(tag & 0x1FFFFFFFu) : -1;
-    if (!valid) vv = INFINITY;
-    #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-        const float v2 = __shfl_down(vv, o, 32);
-        const int j2 = __shfl_down(jb, o, 32);
-        if (c + o < 32 && j2 == jb) vv = fminf(vv, v2);
-    }
-    const int jp = __shfl_up(jb, 1, 32);
-    if (h == 0 && jb >= 0 && (c == 0 || jp != jb)) atomicMin(E.minv + jb, ord_f32(vv));
-}
-
-template <int NT>
-__global__ __launch_bounds__(64 * (slices(NT) / 2)) void k_eval_rw_wide(EvalArgs E) {
-    static_assert(wide_tiles(NT), "wide form");
-    constexpr int NW = slices(NT) / 2, NS = slices(NT);
-    static_assert(NW >= 3, "loader roles need 3 waves");
-    __shared__ StRaw sraw[kRawSlots];
-    __shared__ StRow srow[kRowSlots];
-    __shared__ float part[2][NW][kSetLeaves];
-    __shared__ uint4 utab[256];
-    build_unit_table(utab);
-    const int l = lane_id(), h = l >> 5, c = l & 31, wv = threadIdx.x >> 6;
-    uint4 wh[kKB], wl[kKB];
-    #pragma unroll
-    for (int kb = 0; kb < kKB; ++kb) {
-        wh[kb] = E.w1q[((kb * NS + 2 * wv + 0) * 64) + l];
-        wl[kb] = E.w1q[((kb * NS + 2 * wv + 1) * 64) + l];
-    }
-    float4 hw[4];
-    #pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4) hw[r4] = reinterpret_cast<const float4*>(E.wvq)[(wv * 4 + r4) * 64 + l];
-    const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
-    Stager st{sraw, srow, &E, (long long)(*E.lo / kSetLeaves) + blockIdx.x, (long long)gridDim.x,
-              (long long)(used / kSetLeaves), wv, l, {}, {}, 0u, 0u, 0u, 0u};
-    st.prologue();
-    if (!st.live(0)) return;                          // the whole workgroup (uniform)
-    auto finish = [&](int k) {                        // set k's parts are complete: wave n -> leaf tile n
-        for (int n = wv; n < kSetTiles; n += NW) {
-            const int li = 32 * n + c;
-            float vv = part[k & 1][0][li];
-            #pragma unroll
-            for (int t = 1; t < NW; ++t) vv += part[k & 1][t][li];
-            finish_leaf(E, st.raw(k), st.row(k), li, c, h, vv + E.bv);
-        }
-    };
-    int i = 0;
-    for (; st.live(i); ++i) {
-        st.land(i);
-        if (i > 0) finish(i - 1);
-        st.issue(i);
-        const StRaw& r = st.raw(i);
-        const StRow& w = st.row(i);
-        #pragma unroll 1
-        for (int n = 0; n < kSetTiles; ++n) {
-            const Leaf L = leaf_from_lds(r, w, 32 * n + c);
-            f32x16 x;
-            #pragma unroll
-            for (int kb = 0; kb < kKB; ++kb) {
-                const f16x8 f = feat16t(L, kb, h, utab);
-                x = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wh[kb]), f,
-                                                           kb == 0 ? (f32x16){} : x, 0, 0, 0);
-                x = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wl[kb]), f, x, 0, 0, 0);
-            }
-            float a = 0.0f;
-            #pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-                a = fmaf(relu_raw(x[4 * r4 + 0]), hw[r4].x, a);
-                a = fmaf(relu_raw(x[4 * r4 + 1]), hw[r4].y, a);
-                a = fmaf(relu_raw(x[4 * r4 + 2]), hw[r4].z, a);
-                a = fmaf(relu_raw(x[4 * r4 + 3]), hw[r4].w, a);
-            }
-            a += __shfl_xor(a, 32);
-            if (h == 0) part[i & 1][wv][32 * n + c] = a;
-        }
-    }
-    __syncthreads();                                  // the last set's parts
-    finish(i - 1);
-}
-
-// Narrow form, staged (H <= 48): the same pipeline; a workgroup of 4 waves, wave n
-// holding every unit tile (13 x NT fragments, 156 VGPRs at H = 40) and computing
-// leaf tile n of each set start to end (no parts to exchange).
-template <int NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_eval_rw_narrow(EvalArgs E) {
-    static_assert(NT <= 3, "narrow register form: at most 3 tiles (156 VGPRs of weights)");
-    __shared__ StRaw sraw[kRawSlots];
-    __shared__ StRow srow[kRowSlots];
-    __shared__ float wvs[NT * 8 * 64];
-    __shared__ uint4 utab[256];
-    for (int i = threadIdx.x; i < NT * 8 * 64; i += blockDim.x) wvs[i] = E.wvq[i];
-    build_unit_table(utab);
-    const int l = lane_id(), h = l >> 5, c = l & 31, wv = threadIdx.x >> 6;
-    uint4 wq[NT][kKB];
-    #pragma unroll
-    for (int t = 0; t < NT; ++t)
-        #pragma unroll
-        for (int kb = 0; kb < kKB; ++kb) wq[t][kb] = E.w1q[(kb * NT + t) * 64 + l];
-    const unsigned long long used = *E.hi < E.cap ? *E.hi : E.cap;
-    Stager st{sraw, srow, &E, (long long)(*E.lo / kSetLeaves) + blockIdx.x, (long long)gridDim.x,
-              (long long)(used / kSetLeaves), wv, l, {}, {}, 0u, 0u, 0u, 0u};
-    st.prologue();                                    // (also orders wvs / utab)
-    if (!st.live(0)) return;
-    for (int i = 0; st.live(i); ++i) {
-        st.land(i);
-        st.issue(i);
-        const StRaw& r = st.raw(i);
-        const StRow& w = st.row(i);
-        const int li = 32 * wv + c;
-        const Leaf L = leaf_from_lds(r, w, li);
-        f32x16 x[NT];
-        #pragma unroll
-        for (int kb = 0; kb < kKB; ++kb) {
-            const f16x8 f = feat16t(L, kb, h, utab);
-            #pragma unroll
-            for (int t = 0; t < NT; ++t)
-                x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, wq[t][kb]), f,
-                                                              kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
-        }
-        // hi + lo, relu, times the head weights: two units per packed-fp32 add / fma
-        typedef float f32x2 __attribute__((ext_vector_type(2)));
-        f32x2 v2 = {0.0f, 0.0f};
-        #pragma unroll
-        for (int t = 0; t < NT; ++t)
-            #pragma unroll
-            for (int j = 0; j < 8; j += 2) {
-                const int rr = j < 4 ? j : j + 4;
-                f32x2 u = f32x2{x[t][rr], x[t][rr + 1]} + f32x2{x[t][rr + 4], x[t][rr + 5]};
-                u.x = fmaxf(u.x, 0.0f);
-                u.y = fmaxf(u.y, 0.0f);
-                v2 = __builtin_elementwise_fma(u, f32x2{wvs[(t * 8 + j) * 64 + l], wvs[(t * 8 + j + 1) * 64 + l]}, v2);
-            }
-        float v = v2.x + v2.y;
-        v += __shfl_xor(v, 32) + E.bv;
-        finish_leaf(E, r, w, li, c, h, v);
     }
 }
 
@@ -1249,32 +1288,39 @@ __global__ __launch_bounds__(1024) void k_value_pack16(const float* W1, const fl
     }
 }
 
-// Exclusive scan of the lanes' legal-move counts (one workgroup).
-__global__ __launch_bounds__(1024) void k_scan(Args A, int32_t* lane_off, int64_t* total) {
-    __shared__ int64_t part[1024];
+// Exclusive scan of the lanes' legal-move counts (one workgroup): lane i's rows start at
+// lane_off[i].  by_mover (2-ply): the rows of lanes whose mover is PLAYER1 come first, then
+// PLAYER2's (each group in lane order), so the enumerators' pool output -- every wave walks
+// rows a grid stride apart -- holds long runs of one replier, which the factored evaluator
+// needs per leaf pair (eval_leaves_fact).
+__global__ __launch_bounds__(1024) void k_scan(Args A, int32_t* lane_off, int64_t* total, int by_mover) {
+    __shared__ int64_t part[2][1024];
     const int t = threadIdx.x;
     const int per = (A.B + 1023) / 1024;
     const int lo = t * per, hi = min(A.B, lo + per);
-    int64_t sum = 0;
+    int64_t sum[2] = {0, 0};
     for (int i = lo; i < hi; ++i) {
         const uint8_t* rr = A.lanes + (size_t)i * 64;
-        sum += (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
+        sum[by_mover ? rr[R_CUR] & 1 : 0] += (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
     }
-    part[t] = sum;
+    part[0][t] = sum[0];
+    part[1][t] = sum[1];
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
-        const int64_t v = t >= o ? part[t - o] : 0;
+        const int64_t v0 = t >= o ? part[0][t - o] : 0, v1 = t >= o ? part[1][t - o] : 0;
         __syncthreads();
-        part[t] += v;
+        part[0][t] += v0;
+        part[1][t] += v1;
         __syncthreads();
     }
-    int64_t run = part[t] - sum;
+    int64_t run[2] = {part[0][t] - sum[0], part[0][1023] + part[1][t] - sum[1]};
     for (int i = lo; i < hi; ++i) {
-        lane_off[i] = (int32_t)run;
         const uint8_t* rr = A.lanes + (size_t)i * 64;
-        run += (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
+        const int g = by_mover ? rr[R_CUR] & 1 : 0;
+        lane_off[i] = (int32_t)run[g];
+        run[g] += (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
     }
-    if (t == 1023) *total = part[1023];
+    if (t == 1023) *total = part[0][1023] + part[1][1023];
 }
 
 __global__ void k_expand(Args A, const int32_t* lane_off, int32_t* row_lane) {
@@ -1306,27 +1352,22 @@ static int persistent_grid(const bgx_engine* e, K kernel, int per_cu_cap) {
 typedef void (*EvalFn)(EvalArgs);
 typedef void (*EvalRowsFn)(EvalRowsArgs);
 static int eval_waves(int NT) { return NT <= 4 ? kEvalNarrowWaves : kEvalWideWaves; }
-// the 2-ply evaluator for NT 16-unit slices and its workgroup size: W1 in registers
-// (k_eval_rw_*) except at NT = 4 (208 VGPRs of weights in one wave; LDS weights)
+// the 2-ply evaluator for NT 16-unit slices and its workgroup size; the row-part kernel
 struct EvalPick { EvalFn fn; int threads; };
 static EvalPick eval_kernel(int NT) {
-    if (const char* f = getenv("BGX_EVAL_FORM"); !(f && f[0] == 'r')) {   // default: the LDS-weight form (A/B "r")
-        switch (NT) {
-            case 1: return {k_eval<1>, 64 * eval_waves(1)}; case 2: return {k_eval<2>, 64 * eval_waves(2)};
-            case 3: return {k_eval<3>, 64 * eval_waves(3)}; case 4: return {k_eval<4>, 64 * eval_waves(4)};
-            case 5: return {k_eval<5>, 64 * eval_waves(5)}; case 6: return {k_eval<6>, 64 * eval_waves(6)};
-            case 7: return {k_eval<7>, 64 * eval_waves(7)}; default: return {k_eval<8>, 64 * eval_waves(8)};
-        }
-    }
     switch (NT) {
-        case 1: return {k_eval_rw_narrow<1>, 256};
-        case 2: return {k_eval_rw_narrow<2>, 256};
-        case 3: return {k_eval_rw_narrow<3>, 256};
-        case 4: return {k_eval<4>, 64 * kEvalNarrowWaves};
-        case 5: return {k_eval_rw_wide<5>, 64 * (slices(5) / 2)};
-        case 6: return {k_eval_rw_wide<6>, 64 * (slices(6) / 2)};
-        case 7: return {k_eval_rw_wide<7>, 64 * (slices(7) / 2)};
-        default: return {k_eval_rw_wide<8>, 64 * (slices(8) / 2)};
+        case 1: return {k_eval<1>, 64 * eval_waves(1)}; case 2: return {k_eval<2>, 64 * eval_waves(2)};
+        case 3: return {k_eval<3>, 64 * eval_waves(3)}; case 4: return {k_eval<4>, 64 * eval_waves(4)};
+        case 5: return {k_eval<5>, 64 * eval_waves(5)}; case 6: return {k_eval<6>, 64 * eval_waves(6)};
+        case 7: return {k_eval<7>, 64 * eval_waves(7)}; default: return {k_eval<8>, 64 * eval_waves(8)};
+    }
+}
+typedef void (*RowPartFn)(const uint4*, const int64_t*, const uint4*, float*);
+static RowPartFn rowpart_kernel(int NT) {
+    switch (NT) {
+        case 1: return k_rowpart<1>; case 2: return k_rowpart<2>; case 3: return k_rowpart<3>;
+        case 4: return k_rowpart<4>; case 5: return k_rowpart<5>; case 6: return k_rowpart<6>;
+        case 7: return k_rowpart<7>; default: return k_rowpart<8>;
     }
 }
 static EvalRowsFn eval_rows_kernel(int NT) {
@@ -1396,7 +1437,7 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     uint4* rowkey = (uint4*)(ws + o_key);
     float* vrow = (float*)(ws + o_v);
     const int NT = value_tiles16(hidden);
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, lane_off, total);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, lane_off, total, 0);
     hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
     // ~20 legal moves per lane on average: one wave per ~5 rows at B = 4,096
     const size_t gr = B * 6 < 16384 ? (B * 6 > 64 ? B * 6 : 64) : 16384;
@@ -1442,7 +1483,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     if (rc != BGX_OK) return rc;
     char* ws = (char*)e->search_ws;
     SCK(hipMemsetAsync(ws + o_ctr, 0, 256, s));
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, (int32_t*)ws, (int64_t*)(ws + o_ctr));
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, (int32_t*)ws, (int64_t*)(ws + o_ctr), 1);
     SCK(hipGetLastError());
     int64_t rows64 = 0;
     SCK(hipMemcpyAsync(&rows64, ws + o_ctr, 8, hipMemcpyDeviceToHost, s));
@@ -1451,10 +1492,13 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     if (jobs64 >= (int64_t)0x1FFFFFFF) return BGX_EINVAL;     // job ids are 29-bit pool tags
     const int rows = (int)rows64, jobs = (int)jobs64;
     // [row_lane rows][rowrec rows*64][rowside rows*16][minv jobs*4][maxlen jobs][list jobs*4][retry jobs*4]
+    // [rowpart rows*16*slices f32]
+    const int NT = value_tiles16(hidden);
     const size_t o_rl = head, o_rec = align256(o_rl + (size_t)rows * 4), o_side = align256(o_rec + (size_t)rows * 64),
                  o_minv = align256(o_side + (size_t)rows * 16), o_ml = align256(o_minv + (size_t)jobs * 4),
                  o_list = align256(o_ml + (size_t)jobs), o_retry = align256(o_list + (size_t)jobs * 4),
-                 need = align256(o_retry + (size_t)jobs * 4);
+                 o_rp = align256(o_retry + (size_t)jobs * 4),
+                 need = align256(o_rp + (size_t)rows * 16 * slices(NT) * 4);
     if (e->search_ws_bytes < need) {
         // keep the head (lane_off, counters) across the regrow
         void* nw = nullptr;
@@ -1475,6 +1519,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     uint8_t* maxlen = (uint8_t*)(ws + o_ml);
     int32_t* list = (int32_t*)(ws + o_list);
     int32_t* retry = (int32_t*)(ws + o_retry);
+    float* rowpart = (float*)(ws + o_rp);
 
     if (rows > 0) {
         hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
@@ -1507,10 +1552,16 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             if (const char* c = strchr(fs, ':')) S.cap_mid = atoi(c + 1);
         }
         const bool dbg = getenv("BGX_2PLY_DEBUG") != nullptr;
-        const int NT = value_tiles16(hidden);
         const float* f16s = vpacked;
+        const uint4* w1q = (const uint4*)(f16s + 4);
+        // the root mover's part of X1 per row (the factored evaluator); BGX_2PLY_UNFACTORED
+        // (tests) evaluates every leaf over all 13 k-blocks instead
+        const bool factored = getenv("BGX_2PLY_UNFACTORED") == nullptr;
+        if (factored)
+            hipLaunchKernelGGL(rowpart_kernel(NT), dim3((rows + 127) / 128 < 8192 ? (rows + 127) / 128 : 8192), dim3(256),
+                               0, s, rowside, &ctr->rows, w1q, rowpart);
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
-                   (const uint4*)(f16s + 4), f16s + 4 + kKB * slices(NT) * 64 * 4, value_bias};
+                   w1q, f16s + 4 + kKB * slices(NT) * 64 * 4, value_bias, factored ? rowpart : nullptr, nullptr};
         // the non-doubles enumerator: the row-level walk held to 80 VGPRs (6 waves/SIMD,
         // +1.2 % over its natural 91)
         void (*klight)(S2) = k_enum<kLogLight, -1, 3, 6>;
@@ -1540,6 +1591,12 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         E.keys = S.keys;
         E.tags = S.tags;
         S.cap = E.cap = (unsigned long long)pcap;
+        float* vdbg = nullptr;
+        if (getenv("BGX_2PLY_DUMP")) {
+            SCK(hipMalloc(&vdbg, pcap * 4));
+            SCK(hipMemsetAsync(vdbg, 0, pcap * 4, s));
+            E.vdbg = vdbg;
+        }
         const EvalPick keval = eval_kernel(NT);
         int occ_eval = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ_eval, keval.fn, keval.threads, 0) != hipSuccess ||
@@ -1593,7 +1650,40 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             if (dbg)
                 fprintf(stderr, "[bgx 2-ply] round %d: pool %llu/%zu, tier1 %d, tier2 %d, retry %d, leaves %llu\n", round,
                         hc.cursor, pcap, hc.qcount[0] + hc.qcount[1], hc.qcount[2], hc.retry_count, hc.leaves);
-            if (nretry == 0) break;
+            if (nretry == 0) {
+                // test hook (tests/test_gpu_search.py): per-job minv, row parts, the pool, V per slot
+                if (const char* dp = getenv("BGX_2PLY_DUMP")) {
+                    int32_t* hm = (int32_t*)malloc((size_t)jobs * 4);
+                    SCK(hipMemcpy(hm, minv, (size_t)jobs * 4, hipMemcpyDeviceToHost));
+                    FILE* f = fopen(dp, "wb");
+                    if (f) { fwrite(hm, 4, (size_t)jobs, f); fclose(f); }
+                    free(hm);
+                    const size_t nrp = (size_t)rows * 16 * slices(NT);
+                    float* hr = (float*)malloc(nrp * 4);
+                    SCK(hipMemcpy(hr, rowpart, nrp * 4, hipMemcpyDeviceToHost));
+                    char nm[512];
+                    snprintf(nm, sizeof nm, "%s.rp", dp);
+                    f = fopen(nm, "wb");
+                    if (f) { fwrite(hr, 4, nrp, f); fclose(f); }
+                    free(hr);
+                    const size_t used = hc.cursor < pcap ? hc.cursor : pcap;
+                    auto dumpd = [&](const void* d, size_t bytes, const char* ext) {
+                        void* hb = malloc(bytes);
+                        if (hipMemcpy(hb, d, bytes, hipMemcpyDeviceToHost) == hipSuccess) {
+                            snprintf(nm, sizeof nm, "%s.%s", dp, ext);
+                            if (FILE* g = fopen(nm, "wb")) { fwrite(hb, 1, bytes, g); fclose(g); }
+                        }
+                        free(hb);
+                    };
+                    dumpd(S.keys, used * 16, "keys");
+                    dumpd(S.tags, used * 4, "tags");
+                    dumpd(vdbg, used * 4, "v");
+                    dumpd(rowside, (size_t)rows * 16, "side");
+                    dumpd(maxlen, (size_t)jobs, "ml");
+                    (void)hipFree(vdbg);
+                }
+                break;
+            }
             if (round + 1 >= kMaxRounds) return BGX_ENOMEM;
             // next round: the lost jobs become the explicit list, the pool starts over
             SCK(hipMemcpyAsync(list, retry, (size_t)nretry * 4, hipMemcpyDeviceToDevice, s));

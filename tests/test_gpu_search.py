@@ -167,6 +167,26 @@ def test_two_ply_targeted_roots_vs_oracle(setup, targeted_roots):
     assert big >= 20, big                              # doubles reply sets over 100 moves
 
 
+def test_two_ply_factored_matches_full_form(setup, monkeypatch):
+    """The factored evaluator (the root mover's part of X1 once per row, then the
+    replier's k-blocks, block 12 and the hit deltas per leaf) against the full
+    13-k-block form on every leaf (BGX_2PLY_UNFACTORED): Q within 1e-5, the same
+    surviving-leaf count, the same choice wherever the best Q leads by more than 1e-5."""
+    bgx, net, vh, eng = setup
+    from bgx.search import two_ply
+    best, bestq, q, st = two_ply(eng, vh, want_q=True)
+    monkeypatch.setenv("BGX_2PLY_UNFACTORED", "1")
+    best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
+    assert st2 == st
+    n = eng.n_moves()
+    col = torch.arange(q.shape[1], device="cuda")[None, :]
+    m = col < n[:, None]
+    assert float((q - q2)[m].abs().max()) < TOL
+    qs = torch.where(m, q2, torch.full_like(q2, -1e30)).sort(dim=1, descending=True).values
+    clear = (n > 0) & ((n == 1) | (qs[:, 0] - qs[:, 1] > TOL))
+    assert torch.equal(best[clear], best2[clear])
+
+
 def test_two_ply_pool_retry_rounds(setup, monkeypatch):
     """A leaf pool far too small for one pass: lost jobs are re-run in later
     rounds; Q, the choice and the exact leaf count must not change."""
@@ -236,3 +256,72 @@ def test_two_ply_full_batch_paths_agree(monkeypatch):
     assert bool(torch.isfinite(Q1[col < n[:, None]]).all())
     assert s1["afterstates"] == int(n.sum()) and s1["jobs"] == 21 * s1["afterstates"]
     assert eng.error() == 0
+
+
+def _leaf_reference(net, keys, tags, side, ml):
+    """V of every valid pool leaf in fp64 from its 16-byte key (the replier's nibbles,
+    bar, off, hit mask), its row's mover side and its job's final max length (the
+    evaluator's own inputs, read back from the device): DESIGN.md §5."""
+    used = tags != 0xFFFFFFFF
+    job = (tags & 0x1FFFFFFF).astype(np.int64)
+    valid = used & (ml[np.where(used, job, 0)] == (tags >> 29))
+    idx = np.nonzero(valid)[0]
+    k, jb = keys[idx], job[idx]
+    rs = side[jb // 21]
+    q = ((rs[:, 3] >> 8) & 1).astype(np.int64)
+    hits = k[:, 3] >> 8
+
+    def nib(lo, hi):
+        v = np.zeros((len(lo), 24), np.int64)
+        for p in range(16):
+            v[:, p] = (lo >> np.uint64(4 * p)) & np.uint64(15)
+        for p in range(8):
+            v[:, 16 + p] = (hi >> np.uint32(4 * p)) & np.uint32(15)
+        return v
+    qn = nib(k[:, 0].astype(np.uint64) | (k[:, 1].astype(np.uint64) << np.uint64(32)), k[:, 2])
+    hb = np.stack([(hits >> p) & 1 for p in range(24)], 1).astype(np.int64)
+    mn = nib(rs[:, 0].astype(np.uint64) | (rs[:, 1].astype(np.uint64) << np.uint64(32)), rs[:, 2]) - hb
+    bars = [k[:, 3] & 15, (rs[:, 3] & 15) + hb.sum(1)]
+    offs = [(k[:, 3] >> 4) & 15, (rs[:, 3] >> 4) & 15]
+    F = np.zeros((len(idx), 198))
+    for P in range(2):                           # immutable_board.py:171-212 encoding
+        rep = (q == P)[:, None]
+        cnt = np.where(rep, qn, mn)
+        F[:, 98 * P + 0:96 + 98 * P:4] = cnt >= 1
+        F[:, 98 * P + 1:96 + 98 * P:4] = cnt >= 2
+        F[:, 98 * P + 2:96 + 98 * P:4] = cnt >= 3
+        F[:, 98 * P + 3:96 + 98 * P:4] = np.where(cnt >= 3, (cnt - 3) / 2.0, 0)
+        F[:, 96 + 98 * P] = np.where(q == P, bars[0], bars[1]) / 2.0
+        F[:, 97 + 98 * P] = np.where(q == P, offs[0], offs[1]) / 15.0
+    F[np.arange(len(idx)), 196 + (1 - q)] = 1.0        # the root mover's one-hot
+    W1 = net.fc1.weight.detach().cpu().double().numpy()
+    b1 = net.fc1.bias.detach().cpu().double().numpy()
+    w2 = net.value_head.weight.detach().cpu().double().numpy().ravel()
+    b2 = float(net.value_head.bias.detach().cpu())
+    return idx, np.maximum(F @ W1.T + b1, 0) @ w2 + b2
+
+
+@pytest.mark.parametrize("unfactored", [False, True])
+def test_two_ply_every_leaf_vs_fp64(setup, monkeypatch, tmp_path, unfactored):
+    """Every surviving leaf of the 48-root batch (~534 k): the evaluator's V (the
+    BGX_2PLY_DUMP test hook writes V per pool slot with the pool, row sides and max
+    lengths) against an fp64 MLP on the leaf's own encoding, within 1e-6 -- the factored
+    form (the mover's row part + replier k-blocks + hit deltas) and the full 13-k-block
+    form.  This is the check that found the two-tiles-in-flight wide form wrong on
+    columns 16-31 of its second tile (0.01-0.8 % of leaves, build-dependent)."""
+    bgx, net, vh, eng = setup
+    from bgx.search import two_ply
+    pre = str(tmp_path / "d")
+    monkeypatch.setenv("BGX_2PLY_DUMP", pre)
+    if unfactored:
+        monkeypatch.setenv("BGX_2PLY_UNFACTORED", "1")
+    two_ply(eng, vh)
+    keys = np.fromfile(pre + ".keys", np.uint32).reshape(-1, 4)
+    tags = np.fromfile(pre + ".tags", np.uint32)
+    v = np.fromfile(pre + ".v", np.float32)
+    side = np.fromfile(pre + ".side", np.uint32).reshape(-1, 4)
+    ml = np.fromfile(pre + ".ml", np.uint8)
+    idx, vref = _leaf_reference(net, keys, tags, side, ml)
+    assert len(idx) > 100_000
+    err = np.abs(v[idx].astype(np.float64) - vref)
+    assert err.max() < 1e-6, (int((err > 1e-6).sum()), idx[err > 1e-6][:16] % 64)
