@@ -267,7 +267,8 @@ def test_fused_head_bound_guard_redoes_update():
     assert trs[0].fused_head is False                     # the guard fired
     for a, b in zip(trs[0].net.parameters(), trs[1].net.parameters()):
         assert torch.equal(a, b)
-    assert m0 == m1
+    # the loss parts are fp64 sums of per-workgroup partials (atomic order): equal to 1e-12
+    assert m0.keys() == m1.keys() and all(m0[k] == pytest.approx(m1[k], rel=1e-12, abs=1e-12) for k in m0)
     # and the reference-scale network keeps the fused head
     tr = PPOTrainer(batch=2048, horizon=4, seed=9, chunk=4096)
     tr.iteration()
@@ -289,4 +290,5 @@ def test_lane_returns_kernel_matches_torch_loop():
     g = torch.Generator(device="cuda").manual_seed(1)
     r2 = torch.randn(33, 1000, device="cuda", generator=g)
     d2 = (torch.rand(33, 1000, device="cuda", generator=g) < 0.1).to(torch.uint8)
-    assert torch.equal(lane_returns(r2, d2), _lane_returns_torch(r2, d2))
+    # arbitrary fp32 rewards: the torch ops may round the product differently (within 1 ulp)
+    assert torch.allclose(lane_returns(r2, d2), _lane_returns_torch(r2, d2), rtol=1e-6, atol=1e-6)
