@@ -358,6 +358,34 @@ def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
                                  f"{units}/{hidden} ({tiles}) x 208/198 (K padding, bias as a feature)"}}
 
 
+EVAL_PMC_ARGS = ("--steps 2 --warmup 1 --burn-in 150 --horizon 0 --no-cpu-baseline --two-ply-batches 1 "
+                 "--c2-steps 0 --mirror-steps 0")
+
+
+def enum_roofline(enums, batches_profiled: int, enum_ms: float, src) -> dict:
+    """The 2-ply reply enumeration (k_enum*: the two enumerators side by side on two
+    streams, then the overflow tiers) priced against instruction issue, like the env
+    step's roofline_issue: wave-instructions per batch by pipe (SQ_INSTS_* totals of the
+    committed enum1 pass / the batches that pass ran) over the live enumeration window
+    of this run, against each pipe's chip capacity.  The wave-time split of each
+    enumerator (enum2 pass) says where the rest of its time goes."""
+    model = {"VALU": ("SQ_INSTS_VALU", 2, 1024), "SALU": ("SQ_INSTS_SALU", 1, 256), "LDS": ("SQ_INSTS_LDS", 1, 256),
+             "SMEM": ("SQ_INSTS_SMEM", 1, 256), "VMEM": ("SQ_INSTS_VMEM", 1, 256), "BRANCH": ("SQ_INSTS_BRANCH", 1, 256)}
+    t = enum_ms * 1e-3
+    pipes = {}
+    for p, (c, cyc, units) in model.items():
+        n = sum(e["totals"].get(c, 0.0) for e in enums) / batches_profiled
+        pipes[p] = {"wave_insts_per_batch": n, "achieved_G_per_s": n / t / 1e9, "peak_G_per_s": units * 2.4 / cyc,
+                    "frac": n * cyc / units / 2.4e9 / t}
+    top = max(pipes, key=lambda p: pipes[p]["frac"])
+    return {"kernel": "reply enumeration: " + " + ".join(e["kernel"] for e in enums if e["totals"].get("SQ_INSTS_VALU", 0) > 1e6),
+            "bound": "issue", "pipe": top, "achieved": pipes[top]["achieved_G_per_s"], "peak": pipes[top]["peak_G_per_s"],
+            "unit": "G wave-instructions/s", "frac": pipes[top]["frac"], "pipes": pipes, "enumeration_ms": enum_ms,
+            "wave_time_split": {e["kernel"]: e["wave_time_split"] for e in enums if e.get("wave_time_split")
+                                and e["totals"].get("SQ_INSTS_VALU", 0) > 1e6},
+            "counters_source": src, "batches_profiled": batches_profiled}
+
+
 def policy_roofline(pairs, rows: int, prof, src) -> dict:
     """C3's policy kernel (k_policy_act: encoder + 198->128->{500,1} MLP on split-f16 MFMA +
     masked log-softmax + Gumbel-max sample) priced against the dense MFMA peak: algorithmic
@@ -721,6 +749,12 @@ def main():
                 a2, _, _ = net.act(eng2, seed=5, step=i)
                 eng2.step(a2, want_obs=False, want_info=False)
         line["two_ply"] = two_ply_bench(eng2, args.two_ply_batches, ws, dev)
+        enums = (summ or {}).get("two_ply_enum") if prof_ok else None
+        if enums:
+            # tools/profile.sh's enum passes run --two-ply-batches 1: a warm and a timed batch
+            # at H = 40, then at H = 128 -- 4 enumerations of the same roots
+            line["two_ply"]["roofline_issue"] = enum_roofline(enums, 4, line["two_ply"]["enumeration_ms_per_batch"],
+                                                              summ.get("enum_command", "python bench.py " + EVAL_PMC_ARGS))
         # the same roots with the reference's H = 128 value head (agent/config.py:8)
         line["two_ply_h128"] = two_ply_bench(eng2, 1, ws, dev, hidden=128)
         if eng2 is not engs[0]:             # its 2-ply leaf pool and workspaces (~11 GB) go back
