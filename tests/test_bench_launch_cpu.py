@@ -48,3 +48,19 @@ def test_rank_refuses_world_size_mismatch(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     with pytest.raises(SystemExit, match="WORLD_SIZE=2"):
         b.dist_init(4)
+
+
+def test_enumeration_issue_roofline_from_committed_counters():
+    """two_ply.roofline_issue is reproducible from the committed profile: the
+    enumerators' SQ instruction totals per batch over an enumeration window, priced
+    against each pipe's chip capacity (VALU 2 cycles on 1,024 SIMDs, the rest one per
+    cycle on 256 CUs, 2.4 GHz); the busiest pipe is the roofline."""
+    import json
+    b = _bench()
+    summ = json.load(open(os.path.join(ROOT, "profiles", "latest_summary.json")))
+    enums = summ["two_ply_enum"]
+    r = b.enum_roofline(enums, 4, 26.5, "test")
+    valu = sum(e["totals"]["SQ_INSTS_VALU"] for e in enums) / 4
+    assert r["pipes"]["VALU"]["frac"] == pytest.approx(valu * 2 / 1024 / 2.4e9 / 26.5e-3)
+    assert r["frac"] == max(p["frac"] for p in r["pipes"].values()) and 0 < r["frac"] < 1
+    assert r["pipe"] in ("SALU", "VALU")
