@@ -349,6 +349,16 @@ int bgx_ppo_gw1(const void* dh_dev, const uint8_t* records_dev, int32_t m, int32
 int bgx_lane_returns(const float* rewards_dev, const uint8_t* dones_dev, int32_t T, int32_t B, float gamma,
                      float* out_dev, void* stream);
 
+/* The PPO update's rollout rows in a given order, once per update (the fused head's
+ * row plan, bgx.train.ppo_row_plan; the reference batches memory rows in order,
+ * ppo_agent.py:235-266): row i of each output = row perm[i] of its input, for the
+ * 64-byte records and the four per-row fields (action, old log-prob, return,
+ * advantage).  One kernel (16-byte copies of the records). */
+int bgx_gather_rollout(const int32_t* perm_dev, int32_t n, const uint8_t* records_dev, const int32_t* actions_dev,
+                       const float* old_logp_dev, const float* returns_dev, const float* adv_dev,
+                       uint8_t* records_out, int32_t* actions_out, float* old_logp_out, float* returns_out,
+                       float* adv_out, void* stream);
+
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
  * evaluation after it (k_eval, the MFMA kernel). */

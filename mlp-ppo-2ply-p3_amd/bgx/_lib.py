@@ -73,6 +73,7 @@ SIGNATURES = {
     "bgx_copy_regions": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "bgx_host_device_ptr": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "bgx_lane_returns": (ctypes.c_int, [_P, _P, _I32, _I32, ctypes.c_float, _P, _P]),
+    "bgx_gather_rollout": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),
 }

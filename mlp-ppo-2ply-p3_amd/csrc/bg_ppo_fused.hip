@@ -631,90 +631,135 @@ constexpr int kFB = 7;                      // feature blocks of 32
 constexpr int kW1 = 208;                    // gw1 row width (198 features, ones column, zeros)
 constexpr int kGw1Part = kFB * 32 * kH;     // floats per workgroup partial, [224][128]
 constexpr int kGw1Grid = 512;               // workgroups (2 per CU)
+constexpr int kGw1Rows = 64;                // rows per LDS stage: two 32-row MFMA tiles per barrier
 
-__device__ __forceinline__ void gw1_param(int f, int& byte, float& fa, float& fbias, float& fc) {
-    byte = 0; fa = 0.0f; fbias = 0.0f; fc = 0.0f;
+// Every feature but off / 15 is exact in f16 arithmetic on t = 1024 + v (f16 has unit
+// spacing at 1024): u = min(max(t A + B, 0), C) with n >= k: (1, -1024 - k, 1);
+// (n - 3) / 2: (1/2, -513.5, 64); bar / 2: (1/2, -512, 64); mover one-hot f196:
+// (-1, 1025, 1), f197: (1, -1024, 1); the ones column: (0, 1, 1); padding: 0.
+// off / 15 (fp16(v * fp32(1/15)), as autocast casts fp32 v / 15) stays on the fp32 path.
+__device__ __forceinline__ void gw1_param(int f, int& byte, float& fa, float& fbias, float& fc, bool& off) {
+    byte = 0; fa = 0.0f; fbias = 0.0f; fc = 0.0f; off = false;
     if (f < 196) {
         const int p = f >= 98 ? 1 : 0, q = f - 98 * p;
         if (q < 96) {
             const int k = q & 3;
             byte = 24 * p + (q >> 2);
-            if (k < 3) { fa = 1.0f; fbias = -(float)k; fc = 1.0f; }
-            else { fa = 0.5f; fbias = -1.5f; fc = 64.0f; }
-        } else if (q == 96) { byte = 48 + p; fa = 0.5f; fc = 64.0f; }
-        else { byte = 50 + p; fa = 1.0f / 15.0f; fc = 1.0f; }
-    } else if (f < 198) { byte = 52; fa = f == 196 ? -1.0f : 1.0f; fbias = f == 196 ? 1.0f : 0.0f; fc = 1.0f; }
+            if (k < 3) { fa = 1.0f; fbias = -1024.0f - (float)k; fc = 1.0f; }
+            else { fa = 0.5f; fbias = -513.5f; fc = 64.0f; }
+        } else if (q == 96) { byte = 48 + p; fa = 0.5f; fbias = -512.0f; fc = 64.0f; }
+        else { byte = 50 + p; off = true; }
+    } else if (f < 198) { byte = 52; fa = f == 196 ? -1.0f : 1.0f; fbias = f == 196 ? 1025.0f : -1024.0f; fc = 1.0f; }
     else if (f == 198) { fbias = 1.0f; fc = 1.0f; }
+}
+
+// the A operand (8 rows of this lane's feature) from two dwords of 4 row bytes each
+__device__ __forceinline__ f16x8 gw1_feats(uint32_t w0, uint32_t w1, f16x2 fa, f16x2 fb, f16x2 fc, bool off) {
+    uint4 r;
+    uint32_t* rp = &r.x;
+    #pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t w = j < 2 ? w0 : w1;
+        // (0x64 | byte 2j', 0x64 | byte 2j'+1) of w -> the f16 pair (1024 + v0, 1024 + v1)
+        const uint32_t tb = __builtin_amdgcn_perm(0x64646464u, w, (j & 1) ? 0x04030402u : 0x04010400u);
+        f16x2 u = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, tb), fa, fb);
+        u = __builtin_elementwise_min(__builtin_elementwise_max(u, (f16x2){(_Float16)0.0f, (_Float16)0.0f}), fc);
+        rp[j] = __builtin_bit_cast(uint32_t, u);
+    }
+    if (off) {                                     // lane-divergent: the 2 off features of 224
+        #pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t w = j < 2 ? w0 : w1;
+            const int b0 = 16 * (j & 1);
+            const _Float16 x0 = (_Float16)((float)((w >> b0) & 255u) * (1.0f / 15.0f));
+            const _Float16 x1 = (_Float16)((float)((w >> (b0 + 8)) & 255u) * (1.0f / 15.0f));
+            rp[j] = __builtin_bit_cast(uint32_t, (f16x2){x0, x1});
+        }
+    }
+    return __builtin_bit_cast(f16x8, r);
 }
 
 struct Gw1Args {
     const _Float16* dh;         // [m][128]
     const uint8_t* rec;         // [m][64], the same row order
-    int m, tiles_per_wg;
+    int m, stages_per_wg;
     float* part;                // [grid][224][128]
 };
 
-__global__ __launch_bounds__(448) void k_ppo_gw1(Gw1Args a) {
-    __shared__ __attribute__((aligned(16))) uint8_t sdh[2][32 * 256];
-    __shared__ __attribute__((aligned(16))) uint8_t srt[2][56 * 32];
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ppo_gw1(Gw1Args a) {
+    __shared__ __attribute__((aligned(16))) uint8_t sdh[2][kGw1Rows * 256];
+    __shared__ __attribute__((aligned(16))) uint8_t srt[2][56 * kGw1Rows];
     const int tid = threadIdx.x, fb = tid >> 6, hh = (tid >> 5) & 1;
-    const int ntiles = (a.m + 31) >> 5;
-    const int t0 = blockIdx.x * a.tiles_per_wg, t1 = min(t0 + a.tiles_per_wg, ntiles);
+    const int nst = (a.m + kGw1Rows - 1) / kGw1Rows;
+    const int t0 = blockIdx.x * a.stages_per_wg, t1 = min(t0 + a.stages_per_wg, nst);
     int byte;
-    float fa, fbias, fc;
-    gw1_param(32 * fb + (tid & 31), byte, fa, fbias, fc);
+    float pa, pb, pc;
+    bool off;
+    gw1_param(32 * fb + (tid & 31), byte, pa, pb, pc, off);
+    const f16x2 fa = {(_Float16)pa, (_Float16)pa}, fbv = {(_Float16)pb, (_Float16)pb}, fc = {(_Float16)pc, (_Float16)pc};
     f32x16 acc[4];
     #pragma unroll
     for (int u = 0; u < 4; ++u)
         #pragma unroll
         for (int i = 0; i < 16; ++i) acc[u][i] = 0.0f;
-    // loaders: dh = 512 16-byte chunks per tile (threads take chunk tid, and tid + 448
-    // for tid < 64); records = 32 rows x 14 dwords (bytes 0..55), one per thread
-    // two tiles in flight: the loads of tile t + 2 are issued while tile t is computed
-    // (one tile ahead left the kernel waiting on HBM latency: 180 us per 2^20 rows)
+    // 8 waves: waves 0-6 own the feature blocks, wave 7 only loads.  Loaders per stage: dh =
+    // 64 rows x 16 chunks of 16 B (chunks tid, tid + 512); records = 64 rows x 14 dwords
+    // (bytes 0..55): dwords tid and, for tid < 384, tid + 512.  Two stages in flight: the
+    // loads of stage t + 2 are issued while stage t is computed.
     const uint4 z4 = make_uint4(0, 0, 0, 0);
-    struct Ld { uint4 d0, d1; uint32_t rw; };
-    const int rr = tid / 14, rwd = tid - 14 * (tid / 14);
-    auto load = [&](int tile) {
-        Ld x{z4, z4, 0u};
-        if (tile >= t1) return x;
-        const int row0 = tile * 32;
-        x.d0 = row0 + (tid >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (tid >> 4)) * kH))[tid & 15] : z4;
-        if (tid < 64) {
-            const int i = tid + 448;
-            x.d1 = row0 + (i >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (i >> 4)) * kH))[i & 15] : z4;
+    struct Ld { uint4 d[2]; uint32_t rw[2]; };
+    auto load = [&](int st) {
+        Ld x{{z4, z4}, {0u, 0u}};
+        if (st >= t1) return x;
+        const int row0 = st * kGw1Rows;
+        #pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int c = tid + 512 * k;
+            x.d[k] = row0 + (c >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (c >> 4)) * kH))[c & 15] : z4;
         }
-        const int gr = row0 + rr < a.m ? row0 + rr : a.m - 1;
-        x.rw = ((const uint32_t*)(a.rec + (size_t)gr * 64))[rwd];
+        #pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int w = tid + 512 * k, r = w / 14, dw = w - 14 * r;
+            if (k == 0 || tid < 384) {
+                const int gr = row0 + r < a.m ? row0 + r : a.m - 1;
+                x.rw[k] = ((const uint32_t*)(a.rec + (size_t)gr * 64))[dw];
+            }
+        }
         return x;
     };
     Ld q0 = load(t0), q1 = load(t0 + 1);
     int buf = 0;
-    for (int tile = t0; tile < t1; ++tile, buf ^= 1) {
-        *(uint4*)(sdh[buf] + swz(tid >> 4, tid & 15)) = q0.d0;
-        if (tid < 64) *(uint4*)(sdh[buf] + swz((tid + 448) >> 4, (tid + 448) & 15)) = q0.d1;
+    for (int st = t0; st < t1; ++st, buf ^= 1) {
         #pragma unroll
-        for (int q = 0; q < 4; ++q) srt[buf][(4 * rwd + q) * 32 + rr] = (uint8_t)(q0.rw >> (8 * q));
+        for (int k = 0; k < 2; ++k) {
+            const int c = tid + 512 * k;
+            *(uint4*)(sdh[buf] + swz(c >> 4, c & 15)) = q0.d[k];
+        }
+        #pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int w = tid + 512 * k, r = w / 14, dw = w - 14 * r;
+            if (k == 0 || tid < 384)
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) srt[buf][(4 * dw + q) * kGw1Rows + r] = (uint8_t)(q0.rw[k] >> (8 * q));
+        }
         __syncthreads();
         q0 = q1;
-        q1 = load(tile + 2);                                // behind this tile's MFMAs
+        q1 = load(st + 2);                                  // behind this stage's MFMAs
+        if (fb == kFB) continue;                            // the loader wave (wave-uniform)
         #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const uint8_t* bp = srt[buf] + byte * 32 + 16 * s + 4 * hh;
-            const uint32_t w0 = *(const uint32_t*)bp, w1 = *(const uint32_t*)(bp + 8);
-            f16x8 A;
+        for (int sub = 0; sub < 2; ++sub)
             #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                A[j] = (_Float16)fminf(fmaxf(fmaf((float)((w0 >> (8 * j)) & 255u), fa, fbias), 0.0f), fc);
-                A[4 + j] = (_Float16)fminf(fmaxf(fmaf((float)((w1 >> (8 * j)) & 255u), fa, fbias), 0.0f), fc);
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const uint8_t* bp = srt[buf] + byte * kGw1Rows + 32 * sub + 16 * s2 + 4 * hh;
+                const f16x8 A = gw1_feats(*(const uint32_t*)bp, *(const uint32_t*)(bp + 8), fa, fbv, fc, off);
+                #pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                        A, tr_operand(sdh[buf], 32 * sub, s2, u, laundered_lane()), acc[u], 0, 0, 0);
             }
-            #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, tr_operand(sdh[buf], 0, s, u, laundered_lane()),
-                                                                acc[u], 0, 0, 0);
-        }
     }
     // C = [32 features][32 units] per u: lane = unit 32u + (l & 31), register i = feature (i&3) + 8(i>>2) + 4hh
+    if (fb == kFB) return;
     float* out = a.part + (size_t)blockIdx.x * kGw1Part;
     #pragma unroll
     for (int u = 0; u < 4; ++u)
@@ -759,6 +804,27 @@ __global__ __launch_bounds__(256) void k_lane_returns(const float* __restrict__ 
         R = __fadd_rn(r[i], __fmul_rn(gamma, R));
         out[i] = R;
     }
+}
+
+// ---- the update's rollout rows in plan order (bgx_gather_rollout): 4 threads per row,
+// each copying 16 bytes of the record; thread 0..3 of a row also copies one of the four
+// per-row fields
+__global__ __launch_bounds__(256) void k_gather_rollout(const int32_t* __restrict__ perm, int n,
+                                                        const uint4* __restrict__ rec, const int32_t* __restrict__ act,
+                                                        const float* __restrict__ old, const float* __restrict__ ret,
+                                                        const float* __restrict__ adv, uint4* __restrict__ rec_o,
+                                                        int32_t* __restrict__ act_o, float* __restrict__ old_o,
+                                                        float* __restrict__ ret_o, float* __restrict__ adv_o) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t i = t >> 2;
+    const int q = (int)(t & 3);
+    if (i >= n) return;
+    const int64_t src = perm[i];
+    rec_o[i * 4 + q] = rec[src * 4 + q];
+    if (q == 0) act_o[i] = act[src];
+    else if (q == 1) old_o[i] = old[src];
+    else if (q == 2) ret_o[i] = ret[src];
+    else adv_o[i] = adv[src];
 }
 
 }  // namespace
@@ -826,8 +892,8 @@ extern "C" int bgx_ppo_gw2(const void* h, const int32_t* perm, const void* stats
 
 extern "C" int64_t bgx_ppo_gw1_workspace(int32_t m) {
     if (m < 0) return BGX_EINVAL;
-    const int64_t ntiles = (m + 31) / 32;
-    const int64_t wgs = ntiles < kGw1Grid ? (ntiles > 0 ? ntiles : 1) : kGw1Grid;
+    const int64_t nst = (m + kGw1Rows - 1) / kGw1Rows;
+    const int64_t wgs = nst < kGw1Grid ? (nst > 0 ? nst : 1) : kGw1Grid;
     return (wgs + kRed) * kGw1Part * (int64_t)sizeof(float);
 }
 
@@ -837,15 +903,33 @@ extern "C" int bgx_ppo_gw1(const void* dh, const uint8_t* records, int32_t m, in
     if (m == 0) return BGX_OK;
     if (!dh || !records || !workspace || !gw1) return BGX_EINVAL;
     if (((uintptr_t)dh | (uintptr_t)records) % 16 || (uintptr_t)workspace % 16) return BGX_EINVAL;
-    const int ntiles = (m + 31) / 32;
-    const int wgs = ntiles < kGw1Grid ? ntiles : kGw1Grid;
-    const int per = (ntiles + wgs - 1) / wgs;
+    const int nst = (m + kGw1Rows - 1) / kGw1Rows;
+    const int wgs = nst < kGw1Grid ? nst : kGw1Grid;
+    const int per = (nst + wgs - 1) / wgs;
     Gw1Args a{(const _Float16*)dh, records, m, per, workspace};
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_ppo_gw1, dim3(wgs), dim3(448), 0, s, a);
+    hipLaunchKernelGGL(k_ppo_gw1, dim3(wgs), dim3(512), 0, s, a);
     float* part2 = workspace + (size_t)wgs * kGw1Part;
     hipLaunchKernelGGL(k_ppo_gw1_sum1, dim3((kGw1Part + 255) / 256, kRed), dim3(256), 0, s, workspace, wgs, part2);
     hipLaunchKernelGGL(k_ppo_gw1_sum2, dim3((kW1 * kH + 255) / 256), dim3(256), 0, s, part2, gw1);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
+extern "C" int bgx_gather_rollout(const int32_t* perm, int32_t n, const uint8_t* records, const int32_t* actions,
+                                  const float* old_logp, const float* returns, const float* adv, uint8_t* records_out,
+                                  int32_t* actions_out, float* old_logp_out, float* returns_out, float* adv_out,
+                                  void* stream) {
+    if (n < 0) return BGX_EINVAL;
+    if (n == 0) return BGX_OK;
+    if (!perm || !records || !actions || !old_logp || !returns || !adv || !records_out || !actions_out ||
+        !old_logp_out || !returns_out || !adv_out)
+        return BGX_EINVAL;
+    if (((uintptr_t)records | (uintptr_t)records_out) % 16) return BGX_EINVAL;
+    const int64_t threads = (int64_t)n * 4;
+    hipLaunchKernelGGL(k_gather_rollout, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       perm, n, (const uint4*)records, actions, old_logp, returns, adv, (uint4*)records_out,
+                       actions_out, old_logp_out, returns_out, adv_out);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }

@@ -1008,19 +1008,23 @@ __global__ __launch_bounds__(256) void k_rowpart(const uint4* rowside, const int
         L.lo[P] = ((uint64_t)rs.y << 32) | rs.x;
         L.hi[P] = rs.z;
         f32x16 x[NA];
-        #pragma unroll
-        for (int kb = 0; kb < 12; ++kb) {
+        // rows are grouped by replier (k_scan by_mover): a tile of one mover runs only its
+        // 6 point k-blocks (the replier's contribute exact zeros), a mixed tile all 12
+        const uint64_t pm = __ballot(in && P == 1), pz = __ballot(in && P == 0);
+        const int kb0 = pm == 0 ? 0 : (pz == 0 ? 6 : 0), kb1 = pz == 0 ? 12 : (pm == 0 ? 6 : 12);
+        #pragma unroll 1
+        for (int kb = kb0; kb < kb1; ++kb) {
             const f16x8 f = __builtin_bit_cast(f16x8, units_pair(kb_byte(L, kb, h)));
             #pragma unroll
             for (int t = 0; t < NA; ++t) {
                 if constexpr (kWide) {
                     const f16x8 ah = __builtin_bit_cast(f16x8, w1q[((kb * NA + t) * 2 + 0) * 64 + l]);
                     const f16x8 al = __builtin_bit_cast(f16x8, w1q[((kb * NA + t) * 2 + 1) * 64 + l]);
-                    x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+                    x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f, kb == kb0 ? (f32x16){} : x[t], 0, 0, 0);
                     x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f, x[t], 0, 0, 0);
                 } else {
                     const f16x8 a = __builtin_bit_cast(f16x8, w1q[(kb * NT + t) * 64 + l]);
-                    x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+                    x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, f, kb == kb0 ? (f32x16){} : x[t], 0, 0, 0);
                 }
             }
         }
@@ -1185,44 +1189,73 @@ __global__ __launch_bounds__(64 * EvalShape<NT>::kWaves) void k_eval_rows(EvalRo
     }
 }
 
-// 1-ply choice per lane: first argmax of V over its rows (values_out row a = V(a)).
-__global__ void k_one_ply_reduce(Args A, const int32_t* lane_off, const float* vrow, int32_t* best, float* bestv,
-                                 float* vout) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// The first argmax of one lane's row values, one wave per lane: lane j of the wave takes
+// rows j, j + 64, ... (value(a) by the caller's functor), keeps its first strict maximum,
+// then a wave reduction by (larger value, then smaller index) -- the sequential scan's
+// "first a with the largest value" (values that never beat -inf, NaN included, never win;
+// then the choice is 0 as in the scan).  Round 3 ran one thread per lane: at C2's
+// B = 4,096 that was 16 workgroups walking ~20-500 rows each (38 us of a 186 us step).
+template <typename F>
+__device__ __forceinline__ void wave_first_argmax(int n, F value, int& best, float& bestv) {
+    float bv = -INFINITY;
+    int ba = 0x7FFFFFFF;
+    for (int a = lane_id(); a < n; a += 64) {
+        const float x = value(a);
+        if (x > bv) { bv = x; ba = a; }
+    }
+    #pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float v2 = __shfl_xor(bv, o);
+        const int a2 = __shfl_xor(ba, o);
+        if (v2 > bv || (v2 == bv && a2 < ba)) { bv = v2; ba = a2; }
+    }
+    best = ba == 0x7FFFFFFF ? 0 : ba;
+    bestv = n ? bv : 0.0f;
+}
+
+// 1-ply choice per lane: first argmax of V over its rows (values_out row a = V(a)); one
+// wave per lane.
+__global__ __launch_bounds__(256) void k_one_ply_reduce(Args A, const int32_t* lane_off, const float* vrow,
+                                                        int32_t* best, float* bestv, float* vout) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= A.B) return;
     const uint8_t* rr = A.lanes + (size_t)i * 64;
     const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
     const float* v = vrow + lane_off[i];
-    float bv = -INFINITY;
-    int ba = 0;
-    for (int a = 0; a < n; ++a) {
+    int ba;
+    float bv;
+    wave_first_argmax(n, [&](int a) {
         const float x = v[a];
         if (vout) vout[(size_t)i * A.max_moves + a] = x;
-        if (x > bv) { bv = x; ba = a; }
+        return x;
+    }, ba, bv);
+    if (lane_id() == 0) {
+        best[i] = ba;
+        if (bestv) bestv[i] = bv;
     }
-    best[i] = ba;
-    if (bestv) bestv[i] = n ? bv : 0.0f;
 }
 
-// Q(a) = sum_r p_r minv[a][r] (fp32, r in roll order), first argmax.
-__global__ void k_two_ply_reduce(Args A, const int32_t* lane_off, const int32_t* minv, int32_t* best, float* bestq,
-                                 float* qout) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// Q(a) = sum_r p_r minv[a][r] (fp32 FMA, r in roll order), first argmax; one wave per lane.
+__global__ __launch_bounds__(256) void k_two_ply_reduce(Args A, const int32_t* lane_off, const int32_t* minv,
+                                                        int32_t* best, float* bestq, float* qout) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= A.B) return;
     const uint8_t* rr = A.lanes + (size_t)i * 64;
     const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
-    float bq = -INFINITY;
-    int ba = 0;
-    for (int a = 0; a < n; ++a) {
+    int ba;
+    float bq;
+    wave_first_argmax(n, [&](int a) {
         const int32_t* mv = minv + ((size_t)lane_off[i] + a) * 21;
         float q = 0.0f;
         for (int r = 0; r < 21; ++r)
             q = fmaf(kRoll0[r] == kRoll1[r] ? 1.0f / 36.0f : 2.0f / 36.0f, unord_f32(mv[r]), q);
         if (qout) qout[(size_t)i * A.max_moves + a] = q;
-        if (q > bq) { bq = q; ba = a; }
+        return q;
+    }, ba, bq);
+    if (lane_id() == 0) {
+        best[i] = ba;
+        if (bestq) bestq[i] = bq;
     }
-    best[i] = ba;
-    if (bestq) bestq[i] = n ? bq : 0.0f;
 }
 
 __device__ __forceinline__ void split16(float x, _Float16& hi, _Float16& lo) {
@@ -1323,12 +1356,15 @@ __global__ __launch_bounds__(1024) void k_scan(Args A, int32_t* lane_off, int64_
     if (t == 1023) *total = part[0][1023] + part[1][1023];
 }
 
-__global__ void k_expand(Args A, const int32_t* lane_off, int32_t* row_lane) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// row -> lane map, one wave per lane (coalesced stores; one thread per lane walked up to
+// 500 rows serially)
+__global__ __launch_bounds__(256) void k_expand(Args A, const int32_t* lane_off, int32_t* row_lane) {
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= A.B) return;
     const uint8_t* rr = A.lanes + (size_t)i * 64;
     const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
-    for (int a = 0; a < n; ++a) row_lane[lane_off[i] + a] = i;
+    const int o = lane_off[i];
+    for (int a = lane_id(); a < n; a += 64) row_lane[o + a] = i;
 }
 
 }  // namespace
@@ -1438,7 +1474,7 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     float* vrow = (float*)(ws + o_v);
     const int NT = value_tiles16(hidden);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, lane_off, total, 0);
-    hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
+    hipLaunchKernelGGL(k_expand, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, row_lane);
     // ~20 legal moves per lane on average: one wave per ~5 rows at B = 4,096
     const size_t gr = B * 6 < 16384 ? (B * 6 > 64 ? B * 6 : 64) : 16384;
     hipLaunchKernelGGL(k_rows, dim3((unsigned)gr), dim3(256), 0, s, A, row_lane, lane_off, total, nullptr, rowside,
@@ -1447,7 +1483,7 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     const EvalRowsArgs E{rowkey, rowside, total, vrow, (const uint4*)(vpacked + 4), vpacked + 4 + kKB * slices(NT) * 64 * 4,
                          value_bias};
     hipLaunchKernelGGL(kr, dim3(eval_grid(e, kr, NT)), dim3(64 * eval_waves(NT)), 0, s, E);
-    hipLaunchKernelGGL(k_one_ply_reduce, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, vrow, best_out,
+    hipLaunchKernelGGL(k_one_ply_reduce, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, vrow, best_out,
                        bestv_out, values_out);
     SCK(hipGetLastError());
     return BGX_OK;
@@ -1522,7 +1558,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     float* rowpart = (float*)(ws + o_rp);
 
     if (rows > 0) {
-        hipLaunchKernelGGL(k_expand, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, row_lane);
+        hipLaunchKernelGGL(k_expand, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, row_lane);
         SCK(hipMemsetAsync(minv, 0x7F, (size_t)jobs * 4, s));
         SCK(hipMemsetAsync(maxlen, 0xFF, (size_t)jobs, s));
         hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
@@ -1692,7 +1728,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             SCK(hipMemsetAsync(ctr->qcount, 0, 16, s));          // qcount[3], retry_count
         }
     }
-    hipLaunchKernelGGL(k_two_ply_reduce, dim3((A.B + 255) / 256), dim3(256), 0, s, A, lane_off, minv, best_out,
+    hipLaunchKernelGGL(k_two_ply_reduce, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, minv, best_out,
                        bestq_out, q_out);
     SCK(hipGetLastError());
     if (stats_host) {

@@ -183,3 +183,19 @@ def test_gw1_from_records_matches_feature_gemm(m):
     for _ in range(2):
         check(L.bgx_ppo_gw1(_p(dh), _p(recs), m, 128, _p(ws), _p(gw1b), s), "bgx_ppo_gw1")
     assert torch.equal(gw1, gw1b)
+
+
+def test_gather_rollout_matches_torch_indexing():
+    """bgx_gather_rollout (the update's rows in plan order, one kernel) == torch
+    indexing of the records and the four per-row fields, bit for bit."""
+    from bgx.train import gather_rollout
+    g = torch.Generator(device="cuda").manual_seed(3)
+    m = 100_003
+    recs = torch.randint(0, 256, (m, 64), dtype=torch.uint8, device="cuda", generator=g)
+    acts = torch.randint(0, 500, (m,), dtype=torch.int32, device="cuda", generator=g)
+    old, R, adv = (torch.randn(m, device="cuda", generator=g) for _ in range(3))
+    perm = torch.randperm(m, device="cuda", generator=g).to(torch.int32)
+    got = gather_rollout(perm, recs, acts, old, R, adv)
+    pl = perm.long()
+    for a, b in zip(got, (recs[pl], acts[pl], old[pl], R[pl], adv[pl])):
+        assert torch.equal(a, b)

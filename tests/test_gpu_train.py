@@ -290,5 +290,8 @@ def test_lane_returns_kernel_matches_torch_loop():
     g = torch.Generator(device="cuda").manual_seed(1)
     r2 = torch.randn(33, 1000, device="cuda", generator=g)
     d2 = (torch.rand(33, 1000, device="cuda", generator=g) < 0.1).to(torch.uint8)
-    # arbitrary fp32 rewards: the torch ops may round the product differently (within 1 ulp)
-    assert torch.allclose(lane_returns(r2, d2), _lane_returns_torch(r2, d2), rtol=1e-6, atol=1e-6)
+    # arbitrary fp32 rewards: both against the fp64 recursion (rounding differences
+    # between the kernel and torch's elementwise ops accumulate over the 33 steps)
+    ref = _lane_returns_torch(r2.double(), d2)
+    for got in (lane_returns(r2, d2), _lane_returns_torch(r2, d2)):
+        assert torch.allclose(got.double(), ref, rtol=1e-5, atol=1e-5)
