@@ -55,9 +55,15 @@ def parse():
                     help="C2: the 4,096 games as S engines on S streams (S=2: +7%% alone, but -45%% after the "
                          "C3/C4 legs have created their streams: more streams than hardware queues)")
     ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--shards", type=int, default=2,
+    ap.add_argument("--shards", type=int, default=4,
                     help="the B games of a GPU as S engines of B/S lanes on S streams, so one shard's policy "
-                         "kernel runs beside the other's env step (MI355X: S=1 170M, S=2 186M, S=4 177M env steps/s)")
+                         "kernel runs beside another's env step.  With --fork-steps off each shard's graph is one "
+                         "linear chain on its own hardware queue (HIP's 4): S=2 341 M, S=4 382 M, S=8 280 M env "
+                         "steps/s at 1,000 steps (DESIGN.md §8 Round 4)")
+    ap.add_argument("--fork-steps", action="store_true",
+                    help="C3: fork each env step's light launch onto the engine's side stream (round 3's layout, "
+                         "best at S=2: 362 M at 1,000 steps but 313 M at 20, its graphs' internal streams share "
+                         "hardware queues with the other shard's)")
     ap.add_argument("--burn-in", type=int, default=150,
                     help="untimed steps before warmup so the game population reaches its steady mix "
                          "(openings are cheaper than mid-game positions)")
@@ -449,6 +455,7 @@ def main():
                        device=dev) for k in range(S)]
     for e in engs:
         e.reset(want_obs=True)
+        e.set_fork(args.fork_steps)
     eng = engs[0]
     torch.manual_seed(0)
     net = PolicyNet(hidden_size=128, action_size=500).to(dev)
@@ -648,14 +655,16 @@ def main():
                    f"C1-on-GPU: B={B} games/GPU random legal policy env.step",
                    "global_batch": B * ws, "games_per_gpu": B, "max_legal_moves": 500,
                    "parallelism": f"dp{ws} (independent game shards)", "shards_per_gpu": S,
-                   "streams_per_gpu": S,
+                   "streams_per_gpu": S, "step_fork": bool(args.fork_steps),
                    "hip_graph": ({"steps_per_graph": G, "replays": args.steps // G, "eager_steps": args.steps % G}
                                  if graphs else None)},
         "roofline": {"kernel": "env step = k_step<0,9,0,false,1> (predicted-doubles prefix) then "
                                "k_step<0,8,0,true,1> (the rest) + k_order_count/scatter + k_movegen_over tiers, "
                                "one wave per game, "
-                               "the light launch on the engine's side stream (event fork-join); HIP events around "
-                               "bgx_step on the shard's stream, per shard of games_per_gpu/shards lanes",
+                               + ("the light launch on the engine's side stream (event fork-join)" if args.fork_steps
+                                  else "both launches on the shard's stream")
+                               + "; HIP events around bgx_step on the shard's stream, per shard of "
+                                 "games_per_gpu/shards lanes",
                      "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": f"bytes per env-step launch (one shard of {Bs} lanes)",
                      "traffic_per_lane_step": traffic / Bs if traffic else None,
@@ -681,8 +690,9 @@ def main():
         torch.cuda.synchronize(dev)
         if graphs:
             # the headline's graphs, each shard's replayed pair followed by ONE copy launch of
-            # that pair's rows (bgx_copy_regions, all 6 fields) on the shard's copy stream; the
-            # copy of pair p runs beside the steps of pair p + 1.  The copy streams are joined
+            # that pair's rows (bgx_copy_regions, all 6 fields), on the shard's stream (linear
+            # shards) or on its copy stream (--fork-steps); the copy of one shard's pair runs
+            # beside the other shards' steps.  The copy streams are joined
             # only when the ring wraps (before a pair's slots are overwritten).  (Round 4 first
             # captured the copy inside each graph as a forked branch: the graph's join then held
             # every pair to its copy, 179 M vs 248 M env steps/s for the eager form.)
@@ -693,10 +703,18 @@ def main():
             torch.cuda.synchronize(dev)
             barrier(ws)
             t0 = time.perf_counter()
+            # linear shards (the default): the copy on the shard's own stream right after its
+            # pair (4 shards = HIP's 4 hardware queues; per-shard copy streams would share
+            # queues with the other shards' steps: 255 vs 167 M env steps/s, gpurun_out r4n)
+            own = not args.fork_steps
             for r in range(nrep):
                 g = r % len(graphs)
                 for k in range(S):
                     with torch.cuda.stream(streams[k]):
+                        if own:
+                            graphs[g][k].replay()
+                            mirrors[k].copy(g * G, G, stream=streams[k])
+                            continue
                         if g == 0 and r > 0:
                             streams[k].wait_stream(copy_streams[k])     # the ring wraps
                         graphs[g][k].replay()
@@ -711,7 +729,8 @@ def main():
             mirror.update({"env_steps_per_s": sum_over_ranks(float(B * msteps), ws) / elm,
                            "ms_per_step": elm * 1e3 / msteps, "steps": msteps,
                            "form": f"the headline's HIP graphs ({G} steps per shard), each replayed pair followed by "
-                                   "one copy launch (6 fields) on the shard's copy stream"})
+                                   "one copy launch (6 fields) on the shard's "
+                                   + ("stream" if own else "copy stream")})
         state["mirror"] = True                       # eager form: one copy launch per step and shard
         esteps = args.mirror_steps if not graphs else min(args.mirror_steps, 16)
         for _ in range(2):

@@ -58,6 +58,15 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
  * calls it before capturing and as its last captured call, so the graph holds no
  * work it does not join. */
 int bgx_engine_join(bgx_engine* e, void* stream);
+/* Where a Philox step's light launch (the non-predicted-doubles rest of the dispatch
+ * order) and the next step's dispatch order run: fork = 1 (default) on the engine's
+ * side stream, fork-joined on events beside the heavy launch; fork = 0 on the caller's
+ * stream after it.  Same results either way.  A HIP graph of fork = 0 steps is one
+ * linear chain: several such engines on their own streams then map one-to-one onto
+ * the hardware queues (bench.py C3: 4 shards), where forked graphs' internal streams
+ * share queues with the other shards' and serialise them.
+ * Turning the fork off joins a pending dispatch order into `stream`. */
+int bgx_engine_set_fork(bgx_engine* e, int32_t fork, void* stream);
 int bgx_engine_destroy(bgx_engine* e);
 
 /* BackgammonEnv.seed (backgammon_env.py:357-363): per-lane MT19937 seeds

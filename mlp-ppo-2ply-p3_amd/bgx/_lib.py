@@ -23,6 +23,7 @@ SIGNATURES = {
     "bgx_engine_create": (ctypes.c_int, [ctypes.c_int, _I32, _I32, ctypes.c_uint64, _I32, _I32, _I32,
                                          ctypes.POINTER(_P)]),
     "bgx_engine_destroy": (ctypes.c_int, [_P]),
+    "bgx_engine_set_fork": (ctypes.c_int, [_P, _I32, _P]),
     "bgx_engine_seed": (ctypes.c_int, [_P, _P, ctypes.c_uint64]),
     "bgx_engine_mt_state": (ctypes.c_int, [_P, _I32, _P, _I32]),
     "bgx_engine_buffers": (ctypes.c_int, [_P, _P]),

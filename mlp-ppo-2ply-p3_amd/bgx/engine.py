@@ -141,6 +141,14 @@ class Engine:
         HIP graph capture of steps and as the capture's last call (bgx_engine_join)."""
         check(self._lib.bgx_engine_join(self._h, self._stream()), "bgx_engine_join")
 
+    def set_fork(self, fork: bool):
+        """fork=True (default): a Philox step's light launch and the next dispatch order
+        run on the engine's side stream beside the heavy launch; False: all of a step
+        on the current stream, so a HIP graph of steps is one linear chain (several
+        engines on their own streams then fill the hardware queues one each; bench.py
+        C3).  Same results either way (bgx_engine_set_fork)."""
+        check(self._lib.bgx_engine_set_fork(self._h, int(bool(fork)), self._stream()), "bgx_engine_set_fork")
+
     # --------------------------------------------------------------- state --
     def lanes(self, lane0: int = 0, n: int | None = None):
         """(records uint8[n,64], moves int64[n,max_moves], n_total int32[n]) copies."""

@@ -526,7 +526,8 @@ class PPOTrainer:
     def __init__(self, batch: int = 65536, horizon: int = 64, hidden: int = 128, n_actions: int = 500,
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
                  chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True,
-                 entropy_anneal: str = "train", shards: int | None = None, graphs: bool | None = None):
+                 entropy_anneal: str = "train", shards: int | None = None, graphs: bool | None = None,
+                 fork: bool | None = None):
         if entropy_anneal not in ("train", "train_single"):
             raise ValueError(f"entropy_anneal must be 'train' or 'train_single', got {entropy_anneal!r}")
         self.entropy_anneal = entropy_anneal
@@ -542,9 +543,12 @@ class PPOTrainer:
         # holds (MASK_SHORTCUT_LIMIT; update() falls back to the exact epoch otherwise)
         self.fused_head = True
         # the B lanes as S engines on S streams (bench.py's C3 layout: one shard's policy
-        # kernel runs beside the other's env step); shard 0 keeps the 1-shard seeds
+        # kernel runs beside another's env step); shard 0 keeps the 1-shard seeds.  4 shards
+        # from 65,536 lanes (one per hardware queue: PPO iteration 133 -> 136 M vs 2)
         if shards is None:
-            shards = 2 if self.dev.type == "cuda" and batch >= 32768 and batch % 256 == 0 else 1
+            cuda = self.dev.type == "cuda"
+            shards = (4 if cuda and batch >= 65536 and batch % 1024 == 0 else
+                      2 if cuda and batch >= 32768 and batch % 256 == 0 else 1)
         if batch % shards:
             raise ValueError(f"batch {batch} is not a multiple of shards {shards}")
         self.S = shards
@@ -560,6 +564,13 @@ class PPOTrainer:
         # shard's copy stream, beside the next pair's steps.
         self.graphs = (self.dev.type == "cuda" and horizon % 2 == 0) if graphs is None else graphs
         self._graphs = None
+        # fork (Engine.set_fork): an env step's light launch on the engine's side stream.
+        # Off by default with graphs: each shard's graph is then one linear chain on its own
+        # hardware queue (forked graphs' internal streams share queues with the other
+        # shards' and serialise them: rollout 9.2 -> 6.3 ms at 65,536 x 32)
+        self.fork = (not self.graphs) if fork is None else bool(fork)
+        for e in self.engs:
+            e.set_fork(self.fork)
         torch.manual_seed(seed)
         self.net = PolicyNet(hidden_size=hidden, action_size=n_actions).to(self.dev)
         if _world(process_group) > 1:
@@ -593,19 +604,26 @@ class PPOTrainer:
             e.reset(want_obs=False)
         self._streams = ([torch.cuda.current_stream(self.dev)] + [torch.cuda.Stream(self.dev) for _ in range(self.S - 1)]
                          if self.dev.type == "cuda" else [None])
-        # per shard: the stream its host copies run on (beside the next steps)
-        self._copy_streams = [torch.cuda.Stream(self.dev) for _ in range(self.S)] if pinned else None
+        # per shard: the stream its host copies run on -- with forked steps a copy stream
+        # beside the next steps; with linear shards the shard's own stream (one hardware
+        # queue per shard; the other shards' steps run beside the copy)
+        self._copy_streams = ([torch.cuda.Stream(self.dev) if self.fork else None for _ in range(self.S)]
+                              if pinned else None)
 
     def _mirror_slots(self, k: int, t0: int, n: int):
         """Shard k's rows of slots [t0, t0 + n) to the pinned host buffers, on the shard's
         copy stream forked from its step stream (joined later by _join_copies)."""
         cs = self._copy_streams[k]
-        cs.wait_stream(torch.cuda.current_stream(self.dev))
         lo = k * (self.B // self.S)
+        if cs is None:                           # linear shards: on the step stream itself
+            self.mirror.copy(t0, n, lo, lo + self.B // self.S, stream=torch.cuda.current_stream(self.dev))
+            return
+        cs.wait_stream(torch.cuda.current_stream(self.dev))
         self.mirror.copy(t0, n, lo, lo + self.B // self.S, stream=cs)
 
     def _join_copies(self, k: int):
-        torch.cuda.current_stream(self.dev).wait_stream(self._copy_streams[k])
+        if self._copy_streams[k] is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self._copy_streams[k])
 
     def _slot(self, k: int, t: int):
         """Shard k's views of rollout slot t (contiguous row ranges)."""

@@ -429,6 +429,7 @@ struct bgx_engine {
     hipStream_t step_side;      // the light launch beside the heavy one, and the next dispatch order
     hipEvent_t step_ev[4];      // fork, light done, heavy done, dispatch order done
     bool order_pending;         // the next step's launches wait for step_ev[3]
+    bool step_fork;             // bgx_engine_set_fork: light launch + dispatch order on step_side
     int32_t* ovf_base;
     int ovf_parity;
     bool ovf_next_zeroed;

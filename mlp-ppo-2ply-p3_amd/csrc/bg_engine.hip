@@ -569,6 +569,7 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     e->device = device;
     e->seed = seed;
     e->order_pending = false;
+    e->step_fork = true;
     Args& A = e->a;
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
@@ -620,6 +621,17 @@ int bgx_engine_join(bgx_engine* e, void* stream) {
         CK(hipStreamWaitEvent((hipStream_t)stream, e->step_ev[3], 0));
         e->order_pending = false;
     }
+    return BGX_OK;
+}
+
+int bgx_engine_set_fork(bgx_engine* e, int32_t fork, void* stream) {
+    if (!e) return BGX_EINVAL;
+    CK(hipSetDevice(e->device));
+    if (!fork && e->order_pending) {         // a pending dispatch order joins `stream` first
+        CK(hipStreamWaitEvent((hipStream_t)stream, e->step_ev[3], 0));
+        e->order_pending = false;
+    }
+    e->step_fork = fork != 0;
     return BGX_OK;
 }
 
@@ -761,7 +773,7 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
         // hardware wave limit, ~5x the resident waves; doubles go to the overflow tiers).
         // Plain stream order -- no cross-stream wait that a serializing tool
         // (profiler) or a shared hardware queue could deadlock.
-        if (heavy < A.B) {
+        if (heavy < A.B && e->step_fork) {
             // fork-join on events: the light launch runs on a side stream beside
             // the heavy one (filling the CUs its tail leaves idle)
             if (!e->step_side) {

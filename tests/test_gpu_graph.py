@@ -21,11 +21,15 @@ def _setup(bgx, seed):
     return net, eng
 
 
-def test_graph_replay_matches_eager_steps():
+@pytest.mark.parametrize("fork", [True, False])
+def test_graph_replay_matches_eager_steps(fork):
+    # fork=False: the captured engine runs each step on one stream (a linear graph,
+    # bench.py's C3 layout) against eager forked steps: the same trajectories
     import bgx
     G = 4
     net, ea = _setup(bgx, 21)
     _, eb = _setup(bgx, 21)
+    eb.set_fork(fork)
     assert torch.equal(ea.records(), eb.records())
     n = ea.batch
     bufs = [dict(act=torch.empty(n, dtype=torch.int32, device="cuda"),

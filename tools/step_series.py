@@ -1,7 +1,8 @@
 """C3 step time against game age: the bench's headline step (B = 65,536 games as
-2 shards on 2 streams, 2-step HIP graphs per shard, policy + masked sampling +
-env.step + rollout rows to the HBM ring) from a fresh reset to --steps steps,
-timed in windows of --window steps with HIP events (the two shards are joined
+--shards shards on their own streams, linear env steps unless --fork, 2-step HIP
+graphs per shard, policy + masked sampling + env.step + rollout rows to the HBM
+ring) from a fresh reset to --steps steps, timed in windows of --window steps with
+HIP events (the shards are joined
 only at window boundaries, as bench.py's timed region is).  Separates the
 population's game-age effect from box-to-box effects.
 
@@ -28,14 +29,17 @@ def main():
     ap.add_argument("--window", type=int, default=20)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--shards", type=int, default=4)
+    ap.add_argument("--fork", action="store_true", help="fork each step's light launch (bench.py --fork-steps)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    S, B, ring, G = 2, args.batch, 32, 2
+    S, B, ring, G = args.shards, args.batch, 32, 2
     Bs = B // S
     engs = [bgx.Engine(batch=Bs, max_moves=500, seed=args.seed + 104729 * k, dice="philox", auto_reset=True,
                        device=dev) for k in range(S)]
     for e in engs:
         e.reset(want_obs=False)
+        e.set_fork(args.fork)
     torch.manual_seed(0)
     net = PolicyNet(hidden_size=128, action_size=500).to(dev)
     net.pack()
@@ -68,17 +72,20 @@ def main():
     torch.cuda.synchronize(dev)
     out, r = [], 0
     for w0 in range(0, args.steps, args.window):
-        streams[0].wait_stream(streams[1])
+        for st in streams[1:]:
+            streams[0].wait_stream(st)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(streams[0])
-        streams[1].wait_stream(streams[0])
+        for st in streams[1:]:
+            st.wait_stream(streams[0])
         for _ in range(args.window // G):
             row = graphs[r % len(graphs)]
             r += 1
             for k in range(S):
                 with torch.cuda.stream(streams[k]):
                     row[k].replay()
-        streams[0].wait_stream(streams[1])
+        for st in streams[1:]:
+            streams[0].wait_stream(st)
         b.record(streams[0])
         out.append((w0, a, b))
         if len(out) % 10 == 0:
@@ -87,7 +94,7 @@ def main():
     torch.cuda.synchronize(dev)
     rows = [{"age": w0, "ms_per_step": a.elapsed_time(b) / args.window,
              "env_steps_per_s": B * args.window / (a.elapsed_time(b) * 1e-3)} for w0, a, b in out]
-    print(json.dumps({"tool": "tools/step_series.py", "batch": B, "shards": S, "window": args.window,
+    print(json.dumps({"tool": "tools/step_series.py", "batch": B, "shards": S, "fork": args.fork, "window": args.window,
                       "steps": args.steps, "time": time.strftime("%Y-%m-%d %H:%M:%S"), "series": rows}))
 
 
