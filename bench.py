@@ -204,12 +204,13 @@ def cpu_baseline(seconds: float):
     return out
 
 
-def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4):
+def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4, streams=None):
     """Full PPO iterations (rollout of `horizon` steps on B lanes + 4-epoch update
-    with the gradient all-reduce across ranks): env steps/s INCLUDING the update."""
+    with the gradient all-reduce across ranks): env steps/s INCLUDING the update.
+    `streams`: the C3 leg's shard streams, reused when the shard counts match."""
     from bgx.train import PPOTrainer
     group = None
-    tr = PPOTrainer(batch=B, horizon=horizon, seed=11, device=dev, process_group=group)
+    tr = PPOTrainer(batch=B, horizon=horizon, seed=11, device=dev, process_group=group, streams=streams)
     tr.iteration()                                   # warm
     torch.cuda.synchronize(dev)
     barrier(ws)
@@ -254,6 +255,7 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     for e in engs:
         e.reset(want_obs=False)
+        e.set_fork(False)          # one stream per step: 43.1 vs 38.9 M forked (profiles/r4_layout/r4o)
     torch.cuda.synchronize(dev)
 
     def step():
@@ -786,7 +788,10 @@ def main():
         line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev, args.c2_shards,
                                                           not args.no_graphs)
     if args.horizon > 0 and args.workload in ("c3", "ppo"):
-        line["ppo_iteration"] = ppo_iteration_bench(B, args.horizon, ws, dev)
+        # the trainer's shards on the C3 leg's streams (one hardware queue each)
+        tr_shards = 4 if B >= 65536 and B % 1024 == 0 else (2 if B >= 32768 and B % 256 == 0 else 1)
+        line["ppo_iteration"] = ppo_iteration_bench(B, args.horizon, ws, dev,
+                                                    streams=streams if len(streams) == tr_shards else None)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

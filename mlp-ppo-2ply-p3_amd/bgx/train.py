@@ -527,7 +527,7 @@ class PPOTrainer:
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
                  chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True,
                  entropy_anneal: str = "train", shards: int | None = None, graphs: bool | None = None,
-                 fork: bool | None = None):
+                 fork: bool | None = None, streams=None):
         if entropy_anneal not in ("train", "train_single"):
             raise ValueError(f"entropy_anneal must be 'train' or 'train_single', got {entropy_anneal!r}")
         self.entropy_anneal = entropy_anneal
@@ -602,8 +602,18 @@ class PPOTrainer:
         self.last_episode_stats = None
         for e in self.engs:
             e.reset(want_obs=False)
-        self._streams = ([torch.cuda.current_stream(self.dev)] + [torch.cuda.Stream(self.dev) for _ in range(self.S - 1)]
-                         if self.dev.type == "cuda" else [None])
+        # `streams`: the S shard streams to use (a process that already runs shards on
+        # streams of its own passes them: HIP maps streams onto its 4 hardware queues in
+        # creation order, and a fresh set created after many others may land two shards
+        # on one queue -- bench.py's PPO leg after the C3/C4/C2 legs: 113 vs 136 M)
+        if streams is not None:
+            if len(streams) != self.S:
+                raise ValueError(f"streams: {len(streams)} given for {self.S} shards")
+            self._streams = list(streams)
+        else:
+            self._streams = ([torch.cuda.current_stream(self.dev)] +
+                             [torch.cuda.Stream(self.dev) for _ in range(self.S - 1)]
+                             if self.dev.type == "cuda" else [None])
         # per shard: the stream its host copies run on -- with forked steps a copy stream
         # beside the next steps; with linear shards the shard's own stream (one hardware
         # queue per shard; the other shards' steps run beside the copy)

@@ -8,3 +8,6 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u tools/step_series.py --steps 1600 --window 20 > $O/series.json 2> $O/series.err || { tail -5 $O/series.err; exit 1; }
 bash tools/profile.sh r4p > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
 tail -40 $O/profile.log
+# keep what comes back under gpurun's 64 MiB: the big raw CSVs compressed
+find gpurun_out/r4p -name '*.csv' -size +1M -exec gzip -9 {} \;
+du -sh gpurun_out/r4p

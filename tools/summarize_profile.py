@@ -95,9 +95,10 @@ for k in kernels:
 lanes_per_shard = None
 if "--batch" in pmc_cmd.split():
     pa = pmc_cmd.split()
-    lanes_per_shard = int(pa[pa.index("--batch") + 1]) // int(pa[pa.index("--shards") + 1] if "--shards" in pa else 2)
-else:
-    lanes_per_shard = 65536 // 2
+    lanes_per_shard = int(pa[pa.index("--batch") + 1]) // int(pa[pa.index("--shards") + 1] if "--shards" in pa else 4)
+else:                                  # bench.py's defaults: 65,536 games as 4 shards (round 4)
+    pa = pmc_cmd.split()
+    lanes_per_shard = 65536 // int(pa[pa.index("--shards") + 1] if "--shards" in pa else 4)
 sq = {}
 for kind in ("sqi", "sqc"):
     rows = pmc_rows(kind)
