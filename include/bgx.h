@@ -363,6 +363,20 @@ int bgx_lane_returns(const float* rewards_dev, const uint8_t* dones_dev, int32_t
  * ppo_agent.py:235-266): row i of each output = row perm[i] of its input, for the
  * 64-byte records and the four per-row fields (action, old log-prob, return,
  * advantage).  One kernel (16-byte copies of the records). */
+/* The PPO optimizer step: torch.optim.Adam(fused=True) (ADAM_MODE::ORIGINAL; no weight
+ * decay, amsgrad or maximize) as GradScaler.step + GradScaler.update drive it
+ * (ppo_agent.py:302-305 `scaler.step(self.optimizer); scaler.update()`), for up to 8
+ * fp32 tensors: params/grads/exp_avg/exp_avg_sq device pointers, steps = each tensor's
+ * fp32 step counter (device scalar), numels element counts (host arrays of n).  With
+ * scale (GradScaler._scale, fp32) non-null: a non-finite scaled gradient anywhere skips
+ * the step (no parameter, moment or counter changes) and backs the scale off; else the
+ * gradients are unscaled in place and the step is taken; growth_tracker (int32) and the
+ * scale follow _amp_update_scale_.  scale = NULL: a plain Adam step.  found: an int32
+ * device flag, zero before the first call (each call leaves it zero). */
+int bgx_adam_step(int32_t n, float* const* params, float* const* grads, float* const* exp_avg,
+                  float* const* exp_avg_sq, float* const* steps, const int64_t* numels, double lr, double beta1,
+                  double beta2, double eps, float* scale, int32_t* growth_tracker, float growth_factor,
+                  float backoff_factor, int32_t growth_interval, int32_t* found, void* stream);
 int bgx_gather_rollout(const int32_t* perm_dev, int32_t n, const uint8_t* records_dev, const int32_t* actions_dev,
                        const float* old_logp_dev, const float* returns_dev, const float* adv_dev,
                        uint8_t* records_out, int32_t* actions_out, float* old_logp_out, float* returns_out,

@@ -486,6 +486,55 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
     wv.grad, bv.grad = gW2[A:A + 1].contiguous(), gb2[A:A + 1].contiguous()
 
 
+def adam_step(optimizer, scaler) -> bool:
+    """`scaler.step(optimizer); scaler.update()` (ppo_agent.py:302-305) for a fused
+    torch.optim.Adam as ONE HIP call (bgx_adam_step: the inf check, the Adam step and the
+    scale update over every tensor's elements in one flat launch each; torch's fused path
+    runs ~4 multi-tensor workgroups over a 90 k-parameter net plus a dozen small ops).
+    The optimizer state and the GradScaler state are torch's own tensors, updated as
+    torch would (tests/test_gpu_train.py::test_adam_step_matches_torch).  Returns False
+    (nothing done) for a configuration it does not restate: the caller then runs torch's."""
+    if not isinstance(optimizer, torch.optim.Adam) or len(optimizer.param_groups) != 1:
+        return False
+    grp = optimizer.param_groups[0]
+    if (grp.get("weight_decay", 0) or grp.get("amsgrad") or grp.get("maximize") or grp.get("capturable")
+            or grp.get("differentiable") or not grp.get("fused") or torch.is_tensor(grp["lr"])):
+        return False
+    ps = [p for p in grp["params"] if p.grad is not None]
+    if not ps or len(ps) > 8 or any(p.dtype != torch.float32 or p.grad.dtype != torch.float32 or not p.is_cuda
+                                    or not p.is_contiguous() or not p.grad.is_contiguous() for p in ps):
+        return False
+    dev = ps[0].device
+    for p in ps:                                     # torch's lazy state (fused: fp32 device step)
+        st = optimizer.state[p]
+        if len(st) == 0:
+            st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+    found = getattr(optimizer, "_bgx_found", None)
+    if found is None or found.device != dev:
+        found = optimizer._bgx_found = torch.zeros(1, dtype=torch.int32, device=dev)
+    use_scale = scaler is not None and scaler.is_enabled()
+    if use_scale:
+        scale, tracker = scaler._scale, scaler._growth_tracker
+        if scale is None or tracker is None:
+            return False
+    n = len(ps)
+    arr = lambda ts: ctypes.cast((ctypes.c_void_p * n)(*[t.data_ptr() for t in ts]), ctypes.c_void_p)
+    st = [optimizer.state[p] for p in ps]
+    numels = (ctypes.c_int64 * n)(*[p.numel() for p in ps])
+    b1, b2 = grp["betas"]
+    check(_lib.load().bgx_adam_step(
+        n, arr(ps), arr([p.grad for p in ps]), arr([s["exp_avg"] for s in st]), arr([s["exp_avg_sq"] for s in st]),
+        arr([s["step"] for s in st]), ctypes.cast(numels, ctypes.c_void_p), float(grp["lr"]), float(b1), float(b2),
+        float(grp["eps"]), ctypes.c_void_p(scale.data_ptr() if use_scale else None),
+        ctypes.c_void_p(tracker.data_ptr() if use_scale else None),
+        float(scaler._growth_factor) if use_scale else 2.0, float(scaler._backoff_factor) if use_scale else 0.5,
+        int(scaler._growth_interval) if use_scale else 1, ctypes.c_void_p(found.data_ptr()),
+        ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "bgx_adam_step")
+    return True
+
+
 def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync=True, guard=None,
                      fused_head=True):
     dev = next(net.parameters()).device
@@ -512,8 +561,9 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
         out.backward()
     if step:
         allreduce_mean_([p.grad for p in net.parameters() if p.grad is not None], group)
-        scaler.step(optimizer)
-        scaler.update()
+        if not adam_step(optimizer, scaler):
+            scaler.step(optimizer)
+            scaler.update()
     if not sync:        # loss parts stay on the device (fp64, same arithmetic): no host sync per epoch
         m = sums / n_total
         return torch.cat([m, (m[0] + VALUE_LOSS_COEF * m[1] - entropy_coef * m[2]).reshape(1)])

@@ -295,3 +295,46 @@ def test_lane_returns_kernel_matches_torch_loop():
     ref = _lane_returns_torch(r2.double(), d2)
     for got in (lane_returns(r2, d2), _lane_returns_torch(r2, d2)):
         assert torch.allclose(got.double(), ref, rtol=1e-5, atol=1e-5)
+
+
+def test_adam_step_matches_torch():
+    """bgx_adam_step (bgx.train.adam_step) == `scaler.step(opt); scaler.update()` with
+    torch's fused Adam (ppo_agent.py:302-305): parameters, moments, step counters, the
+    unscaled gradients, and the GradScaler scale / growth tracker, over steps that
+    include a non-finite gradient (skipped step, scale backoff) and a growth event."""
+    import copy
+    from torch.amp import GradScaler
+    from bgx.policy import PolicyNet
+    from bgx.train import adam_step
+    torch.manual_seed(3)
+    net_a = PolicyNet(hidden_size=128).cuda()
+    net_b = copy.deepcopy(net_a)
+    opt_a = torch.optim.Adam(net_a.parameters(), lr=1e-3, fused=True)
+    opt_b = torch.optim.Adam(net_b.parameters(), lr=1e-3, fused=True)
+    sc_a, sc_b = GradScaler(device="cuda", growth_interval=3), GradScaler(device="cuda", growth_interval=3)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for it in range(8):
+        sc_a.scale(torch.ones((), device="cuda"))
+        sc_b.scale(torch.ones((), device="cuda"))
+        assert torch.equal(sc_a._scale, sc_b._scale)
+        for pa, pb in zip(net_a.parameters(), net_b.parameters()):
+            gr = torch.randn(pa.shape, device="cuda", generator=g) * sc_a._scale * 1e-2
+            if it == 4 and pa.dim() == 2 and pa.shape[0] == 500:
+                gr[7, 3] = float("inf")
+            pa.grad = gr.clone()
+            pb.grad = gr.clone()
+        sc_a.step(opt_a)
+        sc_a.update()
+        assert adam_step(opt_b, sc_b)
+        torch.cuda.synchronize()
+        assert torch.equal(sc_a._scale, sc_b._scale), it
+        assert torch.equal(sc_a._growth_tracker, sc_b._growth_tracker), it
+        for pa, pb in zip(net_a.parameters(), net_b.parameters()):
+            sa, sb = opt_a.state[pa], opt_b.state[pb]
+            assert torch.equal(sa["step"], sb["step"]), it
+            for k in ("exp_avg", "exp_avg_sq"):
+                assert torch.allclose(sa[k], sb[k], rtol=1e-6, atol=0), (it, k)
+            assert torch.allclose(pa, pb, rtol=1e-6, atol=1e-9), it
+            if it != 4:
+                assert torch.allclose(pa.grad, pb.grad, rtol=1e-6, atol=0), it
+    assert float(sc_a._scale) != 65536.0           # the backoff and growth both happened
