@@ -51,9 +51,9 @@ def parse():
                     help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
     ap.add_argument("--c2-steps", type=int, default=50,
                     help="C2: timed greedy 1-ply self-play steps at B=4096 (0 = skip)")
-    ap.add_argument("--c2-shards", type=int, default=1,
-                    help="C2: the 4,096 games as S engines on S streams (S=2: +7%% alone, but -45%% after the "
-                         "C3/C4 legs have created their streams: more streams than hardware queues)")
+    ap.add_argument("--c2-shards", type=int, default=4,
+                    help="C2: the 4,096 games as S engines on S streams, each replayed as its own HIP graph of "
+                         "linear steps (S=1 43.2 M, S=2 50.0 M, S=4 51.5-52.0 M env steps/s; profiles/r4_layout/r4r)")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--shards", type=int, default=4,
                     help="the B games of a GPU as S engines of B/S lanes on S streams, so one shard's policy "
@@ -237,7 +237,7 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4, stre
     return out
 
 
-def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 2, graphs: bool = True):
+def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 4, graphs: bool = True):
     """C2: B games per GPU, greedy 1-ply self-play with the value head
     MLP(198->40->1): every step = V over each lane's legal afterstates (mover's
     one-hot, as legal_board_features) -> first argmax -> env.step.  The B games
@@ -273,33 +273,37 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
     # is a fixed point of its host state).  Every launch reads its state from the
     # device, so the replays are the same steps as the eager calls.
     graph = None
-    if S == 1 and graphs:
+    if graphs:
         from bgx.graphs import capture
-        # the engine is joined before the capture and as its last call: a step
-        # leaves the next dispatch order on the engine's side stream, which a
-        # capture must not hold unjoined (hipErrorStreamCaptureUnjoined)
-        cap = torch.cuda.Stream(dev)
-        cap.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(cap):
-            engs[0].join()
-            for _ in range(2):
-                best, _ = one_ply(engs[0], vh)
-                engs[0].step(best, want_obs=False, want_info=False)
-            engs[0].join()
+        # each shard's engine is joined before its capture and as the capture's last
+        # call (no side-stream work held unjoined: hipErrorStreamCaptureUnjoined);
+        # one graph per shard, replayed on the shard's stream
+        caps = [torch.cuda.Stream(dev) for _ in range(S)]
+        for k in range(S):
+            caps[k].wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(caps[k]):
+                engs[k].join()
+                for _ in range(2):
+                    best, _ = one_ply(engs[k], vh)
+                    engs[k].step(best, want_obs=False, want_info=False)
+                engs[k].join()
         torch.cuda.synchronize(dev)
 
-        def two_steps():
+        def two_steps(k):
             for _ in range(2):
-                best, _ = one_ply(engs[0], vh)
-                engs[0].step(best, want_obs=False, want_info=False)
-            engs[0].join()
-        graph = capture("c2", two_steps, cap)       # a failed capture ends the process
+                best, _ = one_ply(engs[k], vh)
+                engs[k].step(best, want_obs=False, want_info=False)
+            engs[k].join()
+        # a failed capture ends the process
+        graph = [capture("c2", lambda k=k: two_steps(k), caps[k]) for k in range(S)]
         torch.cuda.synchronize(dev)
     barrier(ws)
     t0 = time.perf_counter()
     if graph is not None:
         for _ in range(steps // 2):
-            graph.replay()
+            for k in range(S):
+                with torch.cuda.stream(streams[k]):
+                    graph[k].replay()
         steps = steps // 2 * 2
     else:
         for _ in range(steps):
