@@ -193,7 +193,7 @@ class _PPOHead(torch.autograd.Function):
 
 def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_coef: float, group=None,
               amp: bool = True, fused: bool | None = None, step: bool = True, sync: bool = True, guard=None,
-              fused_head: bool = True):
+              fused_head: bool = True, scale_hint=None):
     """One full-batch PPO epoch (ppo_agent.py:268-305) over `chunks` =
     iterable of (features, legal_mask, actions, old_logp, returns, advantages
     [, records]), with gradient accumulation and one all-reduce.  Returns loss
@@ -208,7 +208,7 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
         fused = dev_type == "cuda"
     if fused:
         return _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync, guard,
-                                fused_head)
+                                fused_head, scale_hint)
     for feats, legal, actions, old_logp, returns, adv, *_ in chunks:
         w = feats.shape[0] / n_total
         with autocast(device_type=dev_type, enabled=amp):
@@ -536,11 +536,17 @@ def adam_step(optimizer, scaler) -> bool:
 
 
 def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync=True, guard=None,
-                     fused_head=True):
+                     fused_head=True, scale_hint=None):
+    """scale_hint (PPOTrainer.update): {"scale", "tracker"}, the host's copy of the
+    GradScaler state, used instead of get_scale() (a host sync per epoch that left the
+    GPU idle while the next epoch's launches were issued) and advanced as a finite
+    step advances it; the trainer checks it against the device state after the
+    update and redoes the update with per-epoch get_scale() when a skipped
+    (non-finite) step made them differ."""
     dev = next(net.parameters()).device
     if scaler.is_enabled():
         scaler.scale(torch.ones((), device=dev))          # initialises the scale tensor lazily
-        scale = scaler.get_scale()
+        scale = scale_hint["scale"] if scale_hint is not None else scaler.get_scale()
     else:
         scale = 1.0
     sums = torch.zeros(3, dtype=torch.float64, device=dev)
@@ -564,6 +570,12 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
         if not adam_step(optimizer, scaler):
             scaler.step(optimizer)
             scaler.update()
+        if scale_hint is not None and scaler.is_enabled():     # _amp_update_scale_ without a non-finite
+            t = scale_hint["tracker"] + 1
+            if t == scaler._growth_interval:
+                scale_hint["scale"] = float(np.float32(scale_hint["scale"] * scaler._growth_factor))
+                t = 0
+            scale_hint["tracker"] = t
     if not sync:        # loss parts stay on the device (fp64, same arithmetic): no host sync per epoch
         m = sums / n_total
         return torch.cat([m, (m[0] + VALUE_LOSS_COEF * m[1] - entropy_coef * m[2]).reshape(1)])
@@ -801,10 +813,16 @@ class PPOTrainer:
         else:
             snap = self._snapshot()
             guard = torch.zeros((), dtype=torch.bool, device=self.dev)
-            parts = self._epochs(recs, acts, old, R, adv, True, guard)
+            hint = self._scale_state()
+            parts = self._epochs(recs, acts, old, R, adv, True, guard, scale_hint=hint)
             g = guard.to(torch.int32)
             if _world(self.group) > 1:
                 dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.group)
+            if hint is not None and self._scale_state() != hint:
+                # a non-finite step was skipped (the scale backed off on the device): the
+                # later epochs ran at the host's scale; redo the update with get_scale()
+                self._restore(snap)
+                parts = self._epochs(recs, acts, old, R, adv, True, guard)
             if bool(g.item()):               # the masked-action shortcut's bound broke: redo exactly
                 print("[bgx] PPO update: logit bound above the fused head's exact range; update redone on the "
                       "exact epoch, later updates too", flush=True)
@@ -815,7 +833,15 @@ class PPOTrainer:
         p = (parts / NUM_EPOCHS).tolist()
         return {"policy_loss": p[0], "value_loss": p[1], "entropy": p[2], "total_loss": p[3]}
 
-    def _epochs(self, recs, acts, old, R, adv, fused_head: bool, guard=None):
+    def _scale_state(self):
+        """The GradScaler's (scale, growth tracker) on the host (one sync), or None when
+        scaling is off."""
+        if not self.scaler.is_enabled():
+            return None
+        self.scaler.scale(torch.ones((), device=self.dev))     # lazy initialisation
+        return {"scale": float(self.scaler._scale.item()), "tracker": int(self.scaler._growth_tracker.item())}
+
+    def _epochs(self, recs, acts, old, R, adv, fused_head: bool, guard=None, scale_hint=None):
         """The NUM_EPOCHS full-batch epochs of one update; returns the summed loss parts
         (device, fp64)."""
         N = recs.shape[0]
@@ -854,7 +880,8 @@ class PPOTrainer:
         parts = None
         for _ in range(NUM_EPOCHS):
             e = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
-                          amp=self.amp, fused=self.fused, sync=False, guard=guard, fused_head=fused_head)
+                          amp=self.amp, fused=self.fused, sync=False, guard=guard, fused_head=fused_head,
+                          scale_hint=scale_hint)
             parts = e if parts is None else parts + e
         return parts
 
