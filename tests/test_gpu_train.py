@@ -338,3 +338,38 @@ def test_adam_step_matches_torch():
             if it != 4:
                 assert torch.allclose(pa.grad, pb.grad, rtol=1e-6, atol=0), it
     assert float(sc_a._scale) != 65536.0           # the backoff and growth both happened
+
+
+def test_update_redone_after_skipped_step(monkeypatch):
+    """The trainer's host copy of the GradScaler state (no get_scale() sync per epoch):
+    a non-finite gradient in epoch 2 skips that step and backs the scale off on the
+    device, the host copy then differs after the update, and the update is redone
+    from its snapshot with per-epoch get_scale() -- the same weights, Adam state and
+    scale as the exact path run directly."""
+    import bgx.train as T
+    res = []
+    for hinted in (True, False):
+        tr = T.PPOTrainer(batch=2048, horizon=4, seed=3, chunk=8192)
+        tr.rollout()
+        calls = {"n": 0}
+        orig = T.adam_step
+
+        def inj(opt, sc, orig=orig, calls=calls):
+            calls["n"] += 1
+            if calls["n"] % 4 == 2:                    # epoch 2 of every pass
+                opt.param_groups[0]["params"][0].grad[0, 0] = float("inf")
+            return orig(opt, sc)
+        monkeypatch.setattr(T, "adam_step", inj)
+        if not hinted:
+            monkeypatch.setattr(T.PPOTrainer, "_scale_state", lambda self: None)
+        tr.update()
+        torch.cuda.synchronize()
+        res.append(([p.detach().clone() for p in tr.net.parameters()],
+                    [tr.opt.state[p]["exp_avg"].clone() for p in tr.net.parameters()],
+                    float(tr.scaler._scale.item()), calls["n"]))
+        monkeypatch.undo()
+    (pa, ma, sa, na), (pb, mb, sb, nb) = res
+    assert na == 8 and nb == 4                         # hinted: the first pass, then the redo
+    assert sa == sb == 32768.0
+    for a, b in zip(pa + ma, pb + mb):
+        assert torch.allclose(a, b, rtol=1e-6, atol=0)
