@@ -37,8 +37,22 @@ enum bgx_status {
     BGX_EINVAL = -1,     /* bad argument */
     BGX_EDEVICE = -2,    /* HIP error (launch, memory, device selection) */
     BGX_ENOMEM = -3,     /* device allocation failed */
-    BGX_EOVERFLOW = -4   /* a position exceeded the slow-path dedup capacity */
+    BGX_EOVERFLOW = -4,  /* a position exceeded the slow-path dedup capacity */
+    BGX_ESTATE = -5      /* the engine's lanes changed while a call was reading them (see below) */
 };
+
+/* Stream ordering.  Every call that takes a bgx_engine* orders itself after the
+ * engine's previous call: when it comes on a different stream than that call, its
+ * stream first waits (hipStreamWaitEvent) for the previous call's work, so a step on
+ * one stream followed by bgx_two_ply / bgx_one_ply / bgx_copy_lanes / ... on another
+ * reads the lanes the step wrote (the engine's lanes, move lists, overflow queues and
+ * tables and the search workspace are one piece of device state).  Calls captured into
+ * a HIP graph are ordered by the graph: its launch stream must follow whatever else
+ * used the engine, and a call after a graph launch on another stream must be ordered
+ * by the caller.  Kernels that take raw lane pointers (bgx_policy_act*, reading
+ * bgx_buffers.lanes) run on the caller's stream as given.  bgx_two_ply returns
+ * BGX_ESTATE (and bgx_one_ply sets bit 1 of the engine's error word) if it finds a
+ * lane whose legal moves no longer match its row layout, instead of reading past them. */
 
 enum bgx_dice_mode {
     BGX_DICE_MT_LANE = 0,    /* lane i == one BackgammonEnv after env.seed(seeds[i]) (numpy legacy MT19937) */
@@ -179,7 +193,8 @@ int bgx_copy_regions(const bgx_region* regions, int32_t n, int32_t workgroups, v
 int bgx_host_device_ptr(void* host_ptr, void** dev_ptr_out);
 
 /* Sticky device error word (bit 0: a position overflowed the slow-path dedup
- * table).  Synchronises the engine's device. */
+ * table; bit 1: bgx_one_ply found a lane changed under it, see "Stream ordering").
+ * Synchronises the engine's device. */
 int bgx_engine_error(bgx_engine* e, int32_t* err_out);
 
 /* ---- policy network (agent/policy_network.py:44-75) + select_action (ppo_agent.py:138-191) ----

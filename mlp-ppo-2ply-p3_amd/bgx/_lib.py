@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # BGX_LIB overrides the library path (A/B experiments between builds)
 LIB_PATH = os.environ.get("BGX_LIB") or os.path.join(_HERE, "libbgx.so")
 
-BGX_OK, BGX_EINVAL, BGX_EDEVICE, BGX_ENOMEM, BGX_EOVERFLOW = 0, -1, -2, -3, -4
+BGX_OK, BGX_EINVAL, BGX_EDEVICE, BGX_ENOMEM, BGX_EOVERFLOW, BGX_ESTATE = 0, -1, -2, -3, -4, -5
 DICE_MT_LANE, DICE_MT_SHARED, DICE_PHILOX = 0, 1, 2
 
 # (name, restype, argtypes) for every symbol declared in include/bgx.h

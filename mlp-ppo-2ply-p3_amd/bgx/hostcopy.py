@@ -36,6 +36,13 @@ class HostMirror:
         if len(shapes) != 1:
             raise ValueError("HostMirror: every field must be [T, B, ...] with the same T, B")
         self.T, self.B = shapes.pop()
+        for k, v in dev_bufs.items():
+            # bgx_copy_regions moves 16-byte chunks: every lane range's bytes must be a
+            # multiple of 16 (uint8 fields: B a multiple of 16)
+            row = (v[0, 0].numel() if v.dim() > 2 else 1) * v.element_size()
+            if (self.B * row) % 16 or v.data_ptr() % 16:
+                raise ValueError(f"HostMirror: field {k!r} has {self.B * row} bytes per slot; the pinned-host "
+                                 f"copy needs a multiple of 16 (batch a multiple of 16)")
         self.dev = dev_bufs
         self.host = {k: torch.empty(v.shape, dtype=v.dtype).pin_memory() for k, v in dev_bufs.items()}
         self._hptr = {k: host_device_ptr(t) for k, t in self.host.items()}

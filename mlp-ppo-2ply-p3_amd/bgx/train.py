@@ -658,6 +658,9 @@ class PPOTrainer:
                     "dones": torch.empty(T, B, dtype=torch.uint8, **kw)}
         self.pinned = None
         if pinned:                      # the rollout mirrored into pinned host memory
+            if (B // self.S) % 16:
+                raise ValueError(f"pinned=True copies each shard's lanes in 16-byte chunks: the shard batch "
+                                 f"{B // self.S} must be a multiple of 16")
             self.mirror = HostMirror(self.buf)
             self.pinned = self.mirror.host
         self.ep_carry = torch.zeros(B, dtype=torch.float64, **kw)     # train.py:58 episode_rewards
@@ -815,14 +818,16 @@ class PPOTrainer:
             guard = torch.zeros((), dtype=torch.bool, device=self.dev)
             hint = self._scale_state()
             parts = self._epochs(recs, acts, old, R, adv, True, guard, scale_hint=hint)
-            g = guard.to(torch.int32)
-            if _world(self.group) > 1:
-                dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.group)
             if hint is not None and self._scale_state() != hint:
                 # a non-finite step was skipped (the scale backed off on the device): the
                 # later epochs ran at the host's scale; redo the update with get_scale()
                 self._restore(snap)
+                guard.zero_()
                 parts = self._epochs(recs, acts, old, R, adv, True, guard)
+            # the bound check of the update that is kept (after any redo above)
+            g = guard.to(torch.int32)
+            if _world(self.group) > 1:
+                dist.all_reduce(g, op=dist.ReduceOp.MAX, group=self.group)
             if bool(g.item()):               # the masked-action shortcut's bound broke: redo exactly
                 print("[bgx] PPO update: logit bound above the fused head's exact range; update redone on the "
                       "exact epoch, later updates too", flush=True)

@@ -444,4 +444,38 @@ struct bgx_engine {
     float search_ms[2];       // last bgx_two_ply call, round 0: enumeration ms, evaluation ms
     void* oneply_ws;          // bgx_one_ply workspace (rows sized for B x max_moves)
     size_t oneply_ws_bytes;
+    // Cross-stream ordering of the engine's own calls (bgx.h "Stream ordering"): the end of
+    // the last eager call that touched the engine's device state (lanes, moves, overflow
+    // queues and tables, search workspace) and the stream it ran on.  A call on another
+    // stream waits for it first.
+    hipEvent_t use_ev;
+    hipStream_t use_stream;
+    bool use_valid;           // use_ev marks the last call (false: none yet, or it was captured)
+};
+
+// RAII guard of one engine call on stream s: the constructor makes s wait for the engine's
+// previous call when that ran on another stream; the destructor marks this call's end.  A
+// call made while s is being captured into a HIP graph neither waits nor marks (its work
+// runs when the graph is launched; the launch stream orders it): the guard then forgets the
+// last mark, so the next eager call on any stream does not wait on a stale event.
+struct EngineUse {
+    bgx_engine* e;
+    hipStream_t s;
+    bool captured;
+    hipError_t err;
+    EngineUse(bgx_engine* e_, hipStream_t s_) : e(e_), s(s_), captured(false), err(hipSuccess) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) captured = true;
+        if (!captured && e->use_valid && e->use_stream != s) err = hipStreamWaitEvent(s, e->use_ev, 0);
+    }
+    ~EngineUse() {
+        if (captured) { e->use_valid = false; return; }
+        if (!e->use_ev && hipEventCreateWithFlags(&e->use_ev, hipEventDisableTiming) != hipSuccess) {
+            e->use_ev = nullptr;
+            e->use_valid = false;
+            return;
+        }
+        e->use_valid = hipEventRecord(e->use_ev, s) == hipSuccess;
+        e->use_stream = s;
+    }
 };

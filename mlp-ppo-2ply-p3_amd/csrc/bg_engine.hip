@@ -617,6 +617,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
 int bgx_engine_join(bgx_engine* e, void* stream) {
     if (!e) return BGX_EINVAL;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, (hipStream_t)stream);
+    CK(use.err);
     if (e->order_pending) {                  // the next step's dispatch order, on the side stream
         CK(hipStreamWaitEvent((hipStream_t)stream, e->step_ev[3], 0));
         e->order_pending = false;
@@ -627,6 +629,8 @@ int bgx_engine_join(bgx_engine* e, void* stream) {
 int bgx_engine_set_fork(bgx_engine* e, int32_t fork, void* stream) {
     if (!e) return BGX_EINVAL;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, (hipStream_t)stream);
+    CK(use.err);
     if (!fork && e->order_pending) {         // a pending dispatch order joins `stream` first
         CK(hipStreamWaitEvent((hipStream_t)stream, e->step_ev[3], 0));
         e->order_pending = false;
@@ -638,6 +642,8 @@ int bgx_engine_set_fork(bgx_engine* e, int32_t fork, void* stream) {
 int bgx_engine_destroy(bgx_engine* e) {
     if (!e) return BGX_EINVAL;
     (void)hipSetDevice(e->device);
+    if (e->use_valid) (void)hipEventSynchronize(e->use_ev);   // the last call's work is done
+    if (e->use_ev) (void)hipEventDestroy(e->use_ev);
     Args& A = e->a;
     void* ptrs[] = {A.lanes, A.moves, A.n_total, A.mt, A.ctr, A.shared_rolls, e->ovf_base, A.ovf_queue, A.err,
                     e->slow_tables, e->search_ws, e->search_pool, e->oneply_ws, A.stamps, e->perm, A.cls, e->order_cnt};
@@ -715,6 +721,8 @@ int bgx_reset(bgx_engine* e, const uint8_t* lane_mask_dev, float* obs_dev, void*
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, s);
+    CK(use.err);
     if (e->order_pending) {                  // a step's dispatch order still on the side stream
         CK(hipStreamWaitEvent(s, e->step_ev[3], 0));
         e->order_pending = false;
@@ -746,6 +754,8 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, s);
+    CK(use.err);
     if (e->ovf_next_zeroed) {             // the previous step's k_order_count zeroed the other set
         e->ovf_parity ^= 1;
         A.ovf_count = e->ovf_base + 4 * e->ovf_parity;
@@ -843,6 +853,8 @@ int bgx_movegen(bgx_engine* e, const int8_t* boards52_dev, const uint8_t* player
     if (n == 0) return BGX_OK;
     hipStream_t s = (hipStream_t)stream;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, s);
+    CK(use.err);
     CK(hipMemsetAsync(e->a.ovf_count, 0, 16, s));
     LAUNCH_LOG(e, k_movegen, dim3(n), s, boards52_dev, players_dev, dice_dev, n, max_moves, n_moves_dev, n_total_dev,
                moves_dev, e->a.ovf_count, e->a.ovf_queue);
@@ -887,6 +899,8 @@ int bgx_afterstates(bgx_engine* e, int32_t lane0, int32_t nlanes, int8_t* boards
     if (!e || !boards52_dev || lane0 < 0 || nlanes < 0 || lane0 + nlanes > e->a.B) return BGX_EINVAL;
     if (nlanes == 0) return BGX_OK;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, (hipStream_t)stream);
+    CK(use.err);
     hipLaunchKernelGGL(k_legal<0>, dim3(nlanes), dim3(64), 0, (hipStream_t)stream, e->a, lane0, (void*)boards52_dev);
     CKL();
     return BGX_OK;
@@ -896,6 +910,8 @@ int bgx_legal_features(bgx_engine* e, int32_t lane0, int32_t nlanes, float* out_
     if (!e || !out_dev || lane0 < 0 || nlanes < 0 || lane0 + nlanes > e->a.B) return BGX_EINVAL;
     if (nlanes == 0) return BGX_OK;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, (hipStream_t)stream);
+    CK(use.err);
     hipLaunchKernelGGL(k_legal<1>, dim3(nlanes), dim3(64), 0, (hipStream_t)stream, e->a, lane0, (void*)out_dev);
     CKL();
     return BGX_OK;
@@ -905,6 +921,8 @@ int bgx_action_masks(bgx_engine* e, int16_t* counts_dev, float* masks_dev, void*
     if (!e) return BGX_EINVAL;
     if (!counts_dev && !masks_dev) return BGX_OK;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, (hipStream_t)stream);
+    CK(use.err);
     hipLaunchKernelGGL(k_action_masks, dim3(e->a.B), dim3(masks_dev ? 256 : 64), 0, (hipStream_t)stream, e->a,
                        counts_dev, masks_dev);
     CKL();
@@ -918,6 +936,8 @@ int bgx_copy_lanes(bgx_engine* e, int32_t lane0, int32_t n, uint8_t* lanes_dst, 
     hipStream_t s = (hipStream_t)stream;
     const Args& A = e->a;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, s);
+    CK(use.err);
     if (lanes_dst) CK(hipMemcpyAsync(lanes_dst, A.lanes + (size_t)lane0 * 64, (size_t)n * 64, hipMemcpyDeviceToDevice, s));
     if (moves_dst)
         CK(hipMemcpyAsync(moves_dst, A.moves + (size_t)lane0 * A.max_moves, (size_t)n * A.max_moves * 8,
@@ -936,6 +956,8 @@ int bgx_set_lanes_ex(bgx_engine* e, int32_t lane0, int32_t n, const uint8_t* lan
     hipStream_t s = (hipStream_t)stream;
     Args& A = e->a;
     CK(hipSetDevice(e->device));
+    EngineUse use(e, s);
+    CK(use.err);
     CK(hipMemcpyAsync(A.lanes + (size_t)lane0 * 64, lanes_src, (size_t)n * 64, hipMemcpyDeviceToDevice, s));
     if (!regen) return BGX_OK;
     CK(hipMemsetAsync(A.ovf_count, 0, 16, s));

@@ -525,17 +525,31 @@ __global__ __launch_bounds__(64) void k_enum_slow(S2 S, uint4* tables) {
 // enumerators and the mover's side of a (nibbles, bar, off, replier q) for k_eval;
 // rowkey (1-ply, may be null): the replier's side of a as a leaf key (no hits) --
 // the row's "no reply" leaf.  The row count comes from *nrows (k_scan's total).
+// A row whose (lane, move index) is not a legal move of the lane as it stands now -- the
+// lanes changed between k_scan and this kernel, which the engine's stream ordering rules
+// out (bgx.h) -- sets *bad and becomes the empty board's row instead of reading past the
+// lane's move list.
 __global__ __launch_bounds__(256) void k_rows(Args A, const int32_t* row_lane, const int32_t* lane_off,
-                                              const int64_t* nrows, uint8_t* rowrec, uint4* rowside, uint4* rowkey) {
+                                              const int64_t* nrows, uint8_t* rowrec, uint4* rowside, uint4* rowkey,
+                                              int32_t* bad) {
     const int l = lane_id();
     const int nw = gridDim.x * (blockDim.x >> 6);
     const int rows = (int)*nrows;
     for (int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < rows; row += nw) {
         const int lane_g = row_lane[row];
-        const int a = row - lane_off[lane_g];
-        const int bv = load_rec(A, lane_g);
+        bool ok = lane_g >= 0 && lane_g < A.B;
+        const int a = ok ? row - lane_off[lane_g] : 0;
+        int bv = ok ? load_rec(A, lane_g) : 0;
+        if (ok) {
+            const int n = rd(bv, R_NM0) | (rd(bv, R_NM1) << 8);
+            ok = a >= 0 && a < n && a < A.max_moves;
+        }
+        if (!ok) {
+            if (l == 0) atomicOr(bad, 2);
+            bv = 0;
+        }
         const int mover = rd(bv, R_CUR);
-        const uint64_t m = uload64(A.moves + (size_t)lane_g * A.max_moves + a);
+        const uint64_t m = ok ? uload64(A.moves + (size_t)lane_g * A.max_moves + a) : 0ull;
         uint32_t blocked;
         Node s = node_from_bytes(bv, mover, blocked);
         s = apply_move(s, m, mover);
@@ -1213,14 +1227,22 @@ __device__ __forceinline__ void wave_first_argmax(int n, F value, int& best, flo
     bestv = n ? bv : 0.0f;
 }
 
+// a lane's legal-move count, held inside the scanned row range [0, total) (equal to the
+// record's count whenever the lanes did not change since k_scan: bgx.h stream ordering)
+__device__ __forceinline__ int row_count(const uint8_t* rr, int32_t off, int64_t total) {
+    const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
+    const int64_t room = off >= 0 && off <= total ? total - off : 0;
+    return n < room ? n : (int)room;
+}
+
 // 1-ply choice per lane: first argmax of V over its rows (values_out row a = V(a)); one
 // wave per lane.
-__global__ __launch_bounds__(256) void k_one_ply_reduce(Args A, const int32_t* lane_off, const float* vrow,
-                                                        int32_t* best, float* bestv, float* vout) {
+__global__ __launch_bounds__(256) void k_one_ply_reduce(Args A, const int32_t* lane_off, const int64_t* total,
+                                                        const float* vrow, int32_t* best, float* bestv, float* vout) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= A.B) return;
     const uint8_t* rr = A.lanes + (size_t)i * 64;
-    const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
+    const int n = row_count(rr, lane_off[i], *total);
     const float* v = vrow + lane_off[i];
     int ba;
     float bv;
@@ -1236,12 +1258,13 @@ __global__ __launch_bounds__(256) void k_one_ply_reduce(Args A, const int32_t* l
 }
 
 // Q(a) = sum_r p_r minv[a][r] (fp32 FMA, r in roll order), first argmax; one wave per lane.
-__global__ __launch_bounds__(256) void k_two_ply_reduce(Args A, const int32_t* lane_off, const int32_t* minv,
-                                                        int32_t* best, float* bestq, float* qout) {
+__global__ __launch_bounds__(256) void k_two_ply_reduce(Args A, const int32_t* lane_off, const int64_t* total,
+                                                        const int32_t* minv, int32_t* best, float* bestq,
+                                                        float* qout) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= A.B) return;
     const uint8_t* rr = A.lanes + (size_t)i * 64;
-    const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
+    const int n = row_count(rr, lane_off[i], *total);
     int ba;
     float bq;
     wave_first_argmax(n, [&](int a) {
@@ -1358,12 +1381,12 @@ __global__ __launch_bounds__(1024) void k_scan(Args A, int32_t* lane_off, int64_
 
 // row -> lane map, one wave per lane (coalesced stores; one thread per lane walked up to
 // 500 rows serially)
-__global__ __launch_bounds__(256) void k_expand(Args A, const int32_t* lane_off, int32_t* row_lane) {
+__global__ __launch_bounds__(256) void k_expand(Args A, const int32_t* lane_off, const int64_t* total,
+                                                int32_t* row_lane) {
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (i >= A.B) return;
-    const uint8_t* rr = A.lanes + (size_t)i * 64;
-    const int n = (int)rr[R_NM0] | ((int)rr[R_NM1] << 8);
     const int o = lane_off[i];
+    const int n = row_count(A.lanes + (size_t)i * 64, o, *total);
     for (int a = lane_id(); a < n; a += 64) row_lane[o + a] = i;
 }
 
@@ -1451,6 +1474,8 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     if (!e || !vpacked || !best_out || bgx_value_packed_size(hidden) < 0) return BGX_EINVAL;
     SCK(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
+    EngineUse use(e, s);
+    SCK(use.err);
     Args& A = e->a;
     const size_t B = (size_t)A.B, R = B * (size_t)A.max_moves;
     // [lane_off B i32][row total i64][row_lane R i32][rowside R][rowkey R][vrow R f32]: sized for
@@ -1474,16 +1499,16 @@ int bgx_one_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     float* vrow = (float*)(ws + o_v);
     const int NT = value_tiles16(hidden);
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, A, lane_off, total, 0);
-    hipLaunchKernelGGL(k_expand, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, row_lane);
+    hipLaunchKernelGGL(k_expand, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, total, row_lane);
     // ~20 legal moves per lane on average: one wave per ~5 rows at B = 4,096
     const size_t gr = B * 6 < 16384 ? (B * 6 > 64 ? B * 6 : 64) : 16384;
     hipLaunchKernelGGL(k_rows, dim3((unsigned)gr), dim3(256), 0, s, A, row_lane, lane_off, total, nullptr, rowside,
-                       rowkey);
+                       rowkey, A.err);
     const EvalRowsFn kr = eval_rows_kernel(NT);
     const EvalRowsArgs E{rowkey, rowside, total, vrow, (const uint4*)(vpacked + 4), vpacked + 4 + kKB * slices(NT) * 64 * 4,
                          value_bias};
     hipLaunchKernelGGL(kr, dim3(eval_grid(e, kr, NT)), dim3(64 * eval_waves(NT)), 0, s, E);
-    hipLaunchKernelGGL(k_one_ply_reduce, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, vrow, best_out,
+    hipLaunchKernelGGL(k_one_ply_reduce, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, total, vrow, best_out,
                        bestv_out, values_out);
     SCK(hipGetLastError());
     return BGX_OK;
@@ -1494,13 +1519,15 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     if (!e || !vpacked || !best_out || bgx_value_packed_size(hidden) < 0) return BGX_EINVAL;
     SCK(hipSetDevice(e->device));
     hipStream_t s = (hipStream_t)stream;
+    EngineUse use(e, s);
+    SCK(use.err);
     Args& A = e->a;
     const size_t B = (size_t)A.B;
     // workspace head: [lane_off B i32][counters 256 B][overflow queues]
     struct Ctr {
         int64_t rows;
         unsigned long long leaves, cursor;
-        int32_t qcount[3], retry_count, list_count, pad;
+        int32_t qcount[3], retry_count, list_count, bad;    // bad: k_rows found a changed lane
         unsigned long long zero;                      // start of the evaluated pool range
     };
     static_assert(sizeof(Ctr) <= 256, "counters");
@@ -1558,11 +1585,11 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     float* rowpart = (float*)(ws + o_rp);
 
     if (rows > 0) {
-        hipLaunchKernelGGL(k_expand, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, row_lane);
+        hipLaunchKernelGGL(k_expand, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, &ctr->rows, row_lane);
         SCK(hipMemsetAsync(minv, 0x7F, (size_t)jobs * 4, s));
         SCK(hipMemsetAsync(maxlen, 0xFF, (size_t)jobs, s));
         hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
-                           lane_off, &ctr->rows, rowrec, rowside, nullptr);
+                           lane_off, &ctr->rows, rowrec, rowside, nullptr, &ctr->bad);
         SCK(hipGetLastError());
         S2 S{rowrec, 0, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
@@ -1679,6 +1706,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             SCK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, s));
             SCK(hipStreamSynchronize(s));
             const int32_t nretry = hc.retry_count;
+            if (hc.bad) return BGX_ESTATE;     // the lanes changed under the call (bgx.h stream ordering)
             if (round == 0) {
                 SCK(hipEventElapsedTime(&e->search_ms[0], e->search_ev[0], e->search_ev[1]));
                 SCK(hipEventElapsedTime(&e->search_ms[1], e->search_ev[1], e->search_ev[2]));
@@ -1728,7 +1756,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             SCK(hipMemsetAsync(ctr->qcount, 0, 16, s));          // qcount[3], retry_count
         }
     }
-    hipLaunchKernelGGL(k_two_ply_reduce, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, minv, best_out,
+    hipLaunchKernelGGL(k_two_ply_reduce, dim3((A.B + 3) / 4), dim3(256), 0, s, A, lane_off, &ctr->rows, minv, best_out,
                        bestq_out, q_out);
     SCK(hipGetLastError());
     if (stats_host) {

@@ -325,3 +325,45 @@ def test_two_ply_every_leaf_vs_fp64(setup, monkeypatch, tmp_path, unfactored):
     assert len(idx) > 100_000
     err = np.abs(v[idx].astype(np.float64) - vref)
     assert err.max() < 1e-6, (int((err > 1e-6).sum()), idx[err > 1e-6][:16] % 64)
+
+
+def test_two_ply_cross_stream_after_destroyed_engine():
+    """The sequence that faulted in round 4 (profiles/r4_layout/r4v/fault.txt): a
+    65,536-lane engine runs two_ply and is destroyed; two 32,768-lane engines are then
+    stepped on the default stream and, with no host sync, two_ply runs on a fresh
+    non-blocking stream.  The engine orders the call after its own steps (bgx.h "Stream
+    ordering"), so Q, the choices and the surviving-leaf counts equal a same-stream
+    call on the same lanes."""
+    import bgx
+    from bgx.policy import PolicyNet
+    from bgx.search import ValueHead, two_ply
+    torch.manual_seed(0)
+    net = PolicyNet().cuda()
+    vh = ValueHead(PolicyNet(hidden_size=40).cuda())
+
+    def population(n, seed, steps):
+        e = bgx.Engine(batch=n, max_moves=500, seed=seed, dice="philox", auto_reset=True)
+        e.reset(want_obs=False)
+        e.set_fork(False)
+        for i in range(steps):
+            a, _, _ = net.act(net.rollout_inputs(e), seed=5, step=i)
+            e.step(a, want_obs=False, want_info=False)
+        return e
+
+    big = population(65536, 77, 20)
+    two_ply(big, vh)
+    del big
+    torch.cuda.empty_cache()
+    shards = [population(32768, 77 + 7919 * k, 60) for k in range(2)]
+    side = [torch.cuda.Stream() for _ in shards]
+    got = []
+    for e, s in zip(shards, side):                # no sync: the steps may still be running
+        with torch.cuda.stream(s):
+            got.append(two_ply(e, vh, want_q=True))
+    torch.cuda.synchronize()
+    for e, (b1, q1, Q1, s1) in zip(shards, got):
+        b2, q2, Q2, s2 = two_ply(e, vh, want_q=True)
+        assert s1 == s2
+        assert torch.equal(torch.nan_to_num(Q1, 7.0), torch.nan_to_num(Q2, 7.0))
+        assert torch.equal(b1, b2) and torch.equal(q1, q2)
+        assert e.error() == 0

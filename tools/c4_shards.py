@@ -35,6 +35,8 @@ def population(n, seed, dev, steps, net):
 
 def run(engs, vh, batches, dev):
     streams = [torch.cuda.Stream(dev) for _ in engs]
+    for s in streams:               # the populations were stepped on the current stream
+        s.wait_stream(torch.cuda.current_stream(dev))
     for e, s in zip(engs, streams):                  # warm: workspace sizing, code load
         with torch.cuda.stream(s):
             two_ply(e, vh)
@@ -65,7 +67,7 @@ def run(engs, vh, batches, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--shards", type=int, default=2)
+    ap.add_argument("--shards", default="2", help="comma-separated shard counts")
     ap.add_argument("--batches", type=int, default=3)
     ap.add_argument("--hidden", type=int, default=40)
     ap.add_argument("--age", type=int, default=180)
@@ -81,8 +83,11 @@ def main():
     out.append(run(one, vh, a.batches, dev))
     del one
     torch.cuda.empty_cache()
-    sh = [population(a.batch // a.shards, 77 + 7919 * k, dev, a.age, net) for k in range(a.shards)]
-    out.append(run(sh, vh, a.batches, dev))
+    for S in [int(x) for x in a.shards.split(",")]:
+        sh = [population(a.batch // S, 77 + 7919 * k, dev, a.age, net) for k in range(S)]
+        out.append(run(sh, vh, a.batches, dev))
+        del sh
+        torch.cuda.empty_cache()
     print(json.dumps({"tool": "tools/c4_shards.py", "hidden": a.hidden, "runs": out}))
 
 
