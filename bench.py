@@ -49,6 +49,9 @@ def parse():
                     help="also time full PPO iterations (T rollout steps + update); 0 = skip")
     ap.add_argument("--two-ply-batches", type=int, default=2,
                     help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
+    ap.add_argument("--c4-shards", type=int, default=2,
+                    help="C4 (H = 40): the B roots as S engines on S streams and host threads, so one shard's "
+                         "reply enumeration runs beside another's evaluation")
     ap.add_argument("--c2-steps", type=int, default=50,
                     help="C2: timed greedy 1-ply self-play steps at B=4096 (0 = skip)")
     ap.add_argument("--c2-shards", type=int, default=4,
@@ -317,46 +320,106 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
             "steps": steps, "shards": S, "hip_graph": graph is not None}
 
 
-def two_ply_bench(eng, batches: int, ws: int, dev, hidden: int = 40):
+def two_ply_shards(eng, shards: int):
+    """The C4 roots of `eng` as `shards` engines of B/S lanes holding the same positions
+    (records copied, legal moves regenerated: the same rows and leaves as one engine)."""
+    import bgx
+    if shards <= 1 or eng.batch % shards:
+        return [eng]
+    n = eng.batch // shards
+    rec = eng.records()
+    out = []
+    for k in range(shards):
+        e = bgx.Engine(batch=n, max_moves=eng.max_moves, seed=1000 + k, dice="philox", auto_reset=True,
+                       device=eng.device)
+        e.set_lanes(rec[k * n:(k + 1) * n])
+        out.append(e)
+    torch.cuda.synchronize(eng.device)
+    return out
+
+
+def two_ply_bench(engs, batches: int, ws: int, dev, hidden: int = 40):
     """C4: 2-ply expectimax over the 21 rolls for every lane's current position
-    (B roots per GPU), value head MLP(198->H->1) on MFMA."""
+    (B roots per GPU), value head MLP(198->H->1) on MFMA.  The roots run
+    as len(engs) game shards, each on its own stream driven by its own host thread (a
+    bgx_two_ply call synchronises its stream after the row scan and after the pool
+    pass; ctypes drops the GIL inside it), so one shard's reply enumeration runs beside
+    another's evaluation.  Shard k > 0 starts k/S of a batch later."""
+    import threading
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead, two_ply, two_ply_timings
     torch.manual_seed(1)
     vnet = PolicyNet(hidden_size=hidden).to(dev)
     vh = ValueHead(vnet)
-    two_ply(eng, vh)                               # warm (workspace sizing, code load)
+    S = len(engs)
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream(dev))
+    t_warm = 0.0
+    for e, st in zip(engs, streams):               # warm (workspace sizing, code load)
+        with torch.cuda.stream(st):
+            t = time.perf_counter()
+            two_ply(e, vh)
+            t_warm = max(t_warm, time.perf_counter() - t)
     torch.cuda.synchronize(dev)
     barrier(ws)
+    res = [dict(leaves=0, jobs=0, enum_ms=0.0, eval_ms=0.0) for _ in range(S)]
+    errs = []
+
+    def worker(k):
+        try:
+            torch.cuda.set_device(dev)
+            if k:
+                time.sleep(t_warm * k / S)
+            with torch.cuda.stream(streams[k]):
+                for _ in range(batches):
+                    _, _, _, st = two_ply(engs[k], vh)
+                    te, tv = two_ply_timings(engs[k])
+                    r = res[k]
+                    r["leaves"] += st["leaves"]
+                    r["jobs"] += st["jobs"]
+                    r["enum_ms"] += te
+                    r["eval_ms"] += tv
+        except Exception as ex:                   # re-raised in the main thread
+            errs.append(ex)
+
     t0 = time.perf_counter()
-    leaves = jobs = 0
-    enum_ms = eval_ms = 0.0
-    for _ in range(batches):
-        _, _, _, st = two_ply(eng, vh)
-        leaves += st["leaves"]
-        jobs += st["jobs"]
-        te, tv = two_ply_timings(eng)
-        enum_ms += te
-        eval_ms += tv
+    if S == 1:
+        worker(0)
+    else:
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(S)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
     torch.cuda.synchronize(dev)
+    if errs:
+        raise errs[0]
     barrier(ws)
     el = max_over_ranks(time.perf_counter() - t0, ws)
-    roots = sum_over_ranks(float(eng.batch * batches), ws)
+    B = sum(e.batch for e in engs)
+    leaves = sum(r["leaves"] for r in res)
+    jobs = sum(r["jobs"] for r in res)
+    # per-shard HIP-event phase times, averaged over the shards (they overlap)
+    enum_ms = sum(r["enum_ms"] for r in res) / S
+    eval_ms = sum(r["eval_ms"] for r in res) / S
+    roots = sum_over_ranks(float(B * batches), ws)
     leaves_all = sum_over_ranks(float(leaves), ws)
     flop_per_leaf = 2 * 198 * hidden + 2 * hidden
     nt = (hidden + 15) // 16
-    # k_eval (the MFMA kernel): algorithmic FLOPs of its leaves / its HIP-event time
-    eval_tflops = leaves * flop_per_leaf / (eval_ms / batches * 1e-3) / batches / 1e12 if eval_ms > 0 else None
+    # k_eval (the MFMA kernel): algorithmic FLOPs of one shard's leaves / its HIP-event time
+    eval_tflops = (leaves / S) * flop_per_leaf / (eval_ms / batches * 1e-3) / batches / 1e12 if eval_ms > 0 else None
     # evaluator tile forms (DESIGN.md §5): narrow = 16 units (hi + lo rows) per 32-row tile,
     # wide (nt > 4) = 32 units per tile with hi and lo as two k-blocks of one accumulator
     wide = nt > 4
     units = 32 * ((nt + 1) // 2) if wide else 16 * nt
     tiles = (f"H as {(nt + 1) // 2} 32-unit tiles, hi and lo as two k-blocks" if wide
              else f"H as {nt} 16-unit hi+lo tiles")
-    return {"config": f"C4: B={eng.batch} roots/GPU, 2-ply expectimax over 21 rolls, value MLP 198->{hidden}->1 "
+    return {"config": f"C4: B={B} roots/GPU as {S} shard(s) on {S} streams / host threads, 2-ply expectimax over "
+                      f"21 rolls, value MLP 198->{hidden}->1 "
                       "(W1 split hi+lo on f16 MFMA, exact f16 features; fp32-equivalent); leaves encoded with "
                       "the root mover's one-hot, min over replies",
-            "hidden": hidden, "batches": batches,
+            "hidden": hidden, "batches": batches, "shards": S,
             "root_decisions_per_s": roots / el, "leaf_evals_per_s": leaves_all / el,
             "leaves_per_root": leaves_all / roots, "reply_enumerations": jobs * ws, "seconds": el,
             "enumeration_ms_per_batch": enum_ms / batches, "evaluation_ms_per_batch": eval_ms / batches,
@@ -773,15 +836,21 @@ def main():
             for i in range(args.burn_in + args.warmup + args.steps):   # the same game age as shard 0's
                 a2, _, _ = net.act(eng2, seed=5, step=i)
                 eng2.step(a2, want_obs=False, want_info=False)
-        line["two_ply"] = two_ply_bench(eng2, args.two_ply_batches, ws, dev)
+        c4 = two_ply_shards(eng2, args.c4_shards)
+        line["two_ply"] = two_ply_bench(c4, args.two_ply_batches, ws, dev)
+        del c4
+        # the same roots with the reference's H = 128 value head (agent/config.py:8)
+        # (one engine: its phase times are those of a whole B-root batch)
+        line["two_ply_h128"] = two_ply_bench([eng2], 1, ws, dev, hidden=128)
         enums = (summ or {}).get("two_ply_enum") if prof_ok else None
         if enums:
             # tools/profile.sh's enum passes run --two-ply-batches 1: a warm and a timed batch
-            # at H = 40, then at H = 128 -- 4 enumerations of the same roots
-            line["two_ply"]["roofline_issue"] = enum_roofline(enums, 4, line["two_ply"]["enumeration_ms_per_batch"],
-                                                              summ.get("enum_command", "python bench.py " + EVAL_PMC_ARGS))
-        # the same roots with the reference's H = 128 value head (agent/config.py:8)
-        line["two_ply_h128"] = two_ply_bench(eng2, 1, ws, dev, hidden=128)
+            # at H = 40 (as shards), then at H = 128 -- 4 enumerations of the B roots; priced
+            # over the whole-batch enumeration window of the one-engine H = 128 leg (the
+            # enumeration does not depend on H)
+            line["two_ply"]["roofline_issue"] = enum_roofline(
+                enums, 4, line["two_ply_h128"]["enumeration_ms_per_batch"],
+                summ.get("enum_command", "python bench.py " + EVAL_PMC_ARGS))
         if eng2 is not engs[0]:             # its 2-ply leaf pool and workspaces (~11 GB) go back
             del eng2
             import gc

@@ -282,7 +282,8 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
                                            KeySink& sink, unsigned long long& leaves) {
     constexpr uint32_t kAllNd = 0x000B77BEu;        // the 15 non-doubles roll indices
     const int off = (int)((s0.k3 >> 4) & 15u);
-    if ((s0.k3 & 15u) != 0u || 15 - s0.n_home - off < 2) return kAllNd;
+    BG_CNT(1, 1);
+    if ((s0.k3 & 15u) != 0u || 15 - s0.n_home - off < 2) { BG_CNT(3, 1); return kAllNd; }
     const int l = lane_id();
     uint32_t K[7];
     int st[8];
@@ -293,7 +294,7 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
         st[d + 1] = st[d] + __popc(K[d]);
     }
     const int n1 = st[7];
-    if (n1 > 64) return kAllNd;
+    if (n1 > 64) { BG_CNT(3, 1); return kAllNd; }
     // lane l: first sub-move (die dl, source al)
     const bool act = l < n1;
     int dl = 1;
@@ -348,6 +349,7 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
             total += (uint32_t)__popcll(m) << b;
         }
         const int meta = al | (dl << 5) | (r << 8);
+        BG_CNT(5, (total + 63) / 64);
         for (uint32_t ch = 0; ch < total; ch += 64) {
             const uint32_t pp = ch + (uint32_t)l;
             const bool valid = pp < total;
@@ -380,6 +382,8 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
     }
     // every fast roll has a first pass-1 two-step (emitted): max length 2
     const uint32_t fast = kAllNd & ~slow;
+    BG_CNT(4, __popc(slow));
+    BG_CNT(13, emitted);
     if (l < 21 && ((fast >> l) & 1u) && !sink.lost) S.maxlen[job0 + (uint32_t)l] = 2;
     if (!sink.lost) leaves += emitted;
     return slow;
@@ -456,16 +460,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             if (VARIANT == 3) {
                 // the row-level walk; what it leaves (and a lost pool block: the
                 // whole row again) runs per job
+                BG_T0(t0);
                 uint32_t left = nd_row(S, row, sq, q, blocked, sink, leaves);
+                BG_T1(9, t0);
                 if (sink.lost) left = 0x000B77BEu;
+                BG_T0(t1);
                 #pragma unroll 1
                 for (; left; left &= left - 1u) {
                     const int r = __builtin_ctz(left);
                     const int job = row * 21 + r;
+                    BG_CNT(11, 1);
                     done(enum_job<LOG, uint4*, MK, 0>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves), job);
                 }
+                BG_T1(10, t1);
             } else {
                 constexpr int nr = VARIANT == 0 ? 15 : 6;
+                BG_T0(t2);
                 #pragma unroll 1
                 for (int k = 0; k < nr; ++k) {
                     const int r = VARIANT == 0 ? nd_roll(k) : roll_start(k + 1);
@@ -473,6 +483,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                     done(enum_job<LOG, uint4*, MK, VARIANT>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves),
                          job);
                 }
+                BG_T1(12, t2);
             }
             bv = bv_next;
         }
@@ -656,22 +667,32 @@ __device__ __forceinline__ uint32_t f16_pair(uint32_t ab, float s0, float s1) {
 // the four units of two points with counts (a, b) (immutable_board.py:180-195) as
 // f16 pairs [u_k(a), u_k(b)], k = 0..3: n>=1, n>=2, n>=3, (n-3)/2 if n>=3.
 // t = (1024 + a, 1024 + b) in f16 (unit spacing there, so every step is exact):
-// u_k = clamp01(t - 1024 - k) for k < 3 (the VOP3P clamp bit), u_3 = max(t/2 - 513.5, 0).
-// One asm block: its outputs feed MFMA operands, and hipcc's hazard recognizer does
-// not see inside inline asm, so the VALU-write -> MFMA-read wait states (s_nop 1)
-// end the string.
+// u_k = clamp01(t - 1024 - k) for k < 3, u_3 = max(t/2 - 513.5, 0).  Written with
+// builtins: hipcc folds min(max(x, 0), 1) into the VOP3P clamp bit, so this is the same
+// five instructions (3 v_pk_add_f16 clamp, v_pk_fma_f16, v_pk_max_f16) as the round-3/4
+// inline-asm block, but visible to the hazard recognizer.  That block was the cause of the
+// two-tiles-in-flight fault: with accumulators in VGPRs an MFMA may
+// write D to other registers than its C, and the allocator then reused a C register, still
+// being read by the in-flight MFMA (an XDL SrcC read runs over its passes), as an asm output:
+// a VALU write into an in-flight SrcC (WAR) that hipcc pads for its own VALU code but cannot
+// see inside an asm string.
+__device__ __forceinline__ h16x2 clamp01h(h16x2 x) {
+    return __builtin_elementwise_min(__builtin_elementwise_max(x, (h16x2){0, 0}), (h16x2){1, 1});
+}
 __device__ __forceinline__ uint4 units_pair(uint32_t byte) {
-    const uint32_t t = (byte & 15u) | ((byte & 0xF0u) << 12) | 0x64006400u;
-    uint32_t u0, u1, u2, u3;
-    __asm__("v_pk_add_f16 %0, %4, %5 clamp\n\t"
-            "v_pk_add_f16 %1, %4, %6 clamp\n\t"
-            "v_pk_add_f16 %2, %4, %7 clamp\n\t"
-            "v_pk_fma_f16 %3, %4, %8, %9\n\t"
-            "v_pk_max_f16 %3, %3, 0\n\t"
-            "s_nop 1"
-            : "=&v"(u0), "=&v"(u1), "=&v"(u2), "=&v"(u3)
-            : "v"(t), "s"(0xE400E400u), "s"(0xE401E401u), "s"(0xE402E402u), "s"(0x38003800u), "v"(0xE003E003u));
-    return make_uint4(u0, u1, u2, u3);
+    uint32_t tb = (byte & 15u) | ((byte & 0xF0u) << 12) | 0x64006400u;
+    // an empty asm (no instruction, so no hazard) pins where the units are formed: without
+    // it the scheduler hoists the features of later k-blocks and k_eval<3> / k_eval<8>
+    // spill 22 / 14 VGPRs
+    __asm__ volatile("" : "+v"(tb));
+    const h16x2 t = __builtin_bit_cast(h16x2, tb);
+    constexpr _Float16 k0 = -1024.0f, k1 = -1025.0f, k2 = -1026.0f, k3 = -513.5f;
+    const h16x2 u0 = clamp01h(t + (h16x2){k0, k0});
+    const h16x2 u1 = clamp01h(t + (h16x2){k1, k1});
+    const h16x2 u2 = clamp01h(t + (h16x2){k2, k2});
+    const h16x2 u3 = __builtin_elementwise_max(t * (h16x2){0.5f16, 0.5f16} + (h16x2){k3, k3}, (h16x2){0, 0});
+    return make_uint4(__builtin_bit_cast(uint32_t, u0), __builtin_bit_cast(uint32_t, u1),
+                      __builtin_bit_cast(uint32_t, u2), __builtin_bit_cast(uint32_t, u3));
 }
 
 // the two point counts (nibbles) k-block kb < 12 takes from this lane's half h:
@@ -720,50 +741,45 @@ __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0
 // asm would hide the MFMA-result read from the hazard recognizer, which must pad it)
 __device__ __forceinline__ float relu_raw(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
-// Wide tiles (H > 64), one leaf tile of 32 columns at a time.  Two leaf tiles in flight
-// (sharing each weight fragment, 128 accumulator VGPRs at H = 128) gave wrong values in
-// columns 16-31 of the second tile for 0.01-0.8 % of leaves, varying with the build's
-// instruction layout; one tile at a time was exact on every leaf of every build tried
-// (test_two_ply_every_leaf_vs_fp64: all 534 k leaves of a 48-root batch against fp64).
+// Wide tiles (H > 64): both 32-column leaf tiles in flight, sharing every weight fragment
+// (128 accumulator VGPRs at H = 128).
 template <int NT>
-__device__ __forceinline__ float eval_tile_wide(const uint4* wq, const float* wvs, const Leaf& L, int z, float bias) {
+__device__ __forceinline__ void eval_leaves_wide(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z,
+                                                 float bias, float (&v)[2]) {
     constexpr int NW = slices(NT) / 2;
     const int l = lane_id(), h = l >> 5;
-    f32x16 x[NW];
+    f32x16 x[2][NW];
     #pragma unroll
     for (int kb = 0; kb < kKB; ++kb) {
-        const f16x8 f = feat16(L, kb, h);
+        const f16x8 f[2] = {feat16(L[0], kb, h), feat16(L[1], kb, h)};
         #pragma unroll
         for (int t = 0; t < NW; ++t) {
             const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 0) * 64 + l + z]);
             const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 1) * 64 + l + z]);
-            x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
-            x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f, x[t], 0, 0, 0);
+            #pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f[n], kb == 0 ? (f32x16){} : x[n][t], 0, 0, 0);
+                x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f[n], x[n][t], 0, 0, 0);
+            }
         }
     }
     // value head: relu times the head weights, 4 registers' weights per ds_read_b128
-    float a = 0.0f;
+    float a[2] = {0.0f, 0.0f};
     #pragma unroll
     for (int t = 0; t < NW; ++t)
         #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4) {
             const float4 w = reinterpret_cast<const float4*>(wvs)[(t * 4 + r4) * 64 + l + z];
-            a = fmaf(relu_raw(x[t][4 * r4 + 0]), w.x, a);
-            a = fmaf(relu_raw(x[t][4 * r4 + 1]), w.y, a);
-            a = fmaf(relu_raw(x[t][4 * r4 + 2]), w.z, a);
-            a = fmaf(relu_raw(x[t][4 * r4 + 3]), w.w, a);
+            #pragma unroll
+            for (int n = 0; n < 2; ++n) {
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 0]), w.x, a[n]);
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 1]), w.y, a[n]);
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 2]), w.z, a[n]);
+                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 3]), w.w, a[n]);
+            }
         }
-    return a + __shfl_xor(a, 32) + bias;
-}
-
-template <int NT>
-__device__ __forceinline__ void eval_leaves_wide(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z,
-                                                 float bias, float (&v)[2]) {
-    v[0] = eval_tile_wide<NT>(wq, wvs, L[0], z, bias);
-    __builtin_amdgcn_sched_barrier(0);              // the tiles stay apart (not interleaved)
-    int z1 = z;                                     // opaque: the second tile re-reads its fragments
-    __asm__ volatile("" : "+s"(z1));
-    v[1] = eval_tile_wide<NT>(wq, wvs, L[1], z1, bias);
+    #pragma unroll
+    for (int n = 0; n < 2; ++n) v[n] = a[n] + __shfl_xor(a[n], 32) + bias;
 }
 
 template <int NT>
@@ -1119,15 +1135,7 @@ void k_eval(EvalArgs E) {
                 float w[2];
                 int zq = z;                               // opaque per pass: no LDS read hoisted out
                 __asm__ volatile("" : "+s"(zq));
-                if constexpr (wide_tiles(NT)) {         // one leaf tile at a time (eval_tile_wide)
-                    eval_leaves_fact<NT, 1>(wq, wvs, &F[0], zq, E.bv, E.rowpart, qq, &w[0]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    int zr = zq;
-                    __asm__ volatile("" : "+s"(zr));
-                    eval_leaves_fact<NT, 1>(wq, wvs, &F[1], zr, E.bv, E.rowpart, qq, &w[1]);
-                } else {
-                    eval_leaves_fact<NT, 2>(wq, wvs, F, zq, E.bv, E.rowpart, qq, w);
-                }
+                eval_leaves_fact<NT, 2>(wq, wvs, F, zq, E.bv, E.rowpart, qq, w);
                 #pragma unroll
                 for (int n = 0; n < 2; ++n) v[n] = L[n].q == qq ? w[n] : v[n];
             }
@@ -1769,6 +1777,17 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
     }
     return BGX_OK;
 }
+
+#ifdef BGX_COUNTERS
+// this translation unit's work counters (experiments; bg_engine.hip has its own set)
+int bgx_debug_search_counters(unsigned long long* out16) {
+    SCK(hipDeviceSynchronize());
+    SCK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bg::g_cnt), 16 * 8));
+    unsigned long long z[16] = {0};
+    SCK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z, 16 * 8));
+    return BGX_OK;
+}
+#endif
 
 int bgx_two_ply_timings(bgx_engine* e, float* ms2) {
     if (!e || !ms2) return BGX_EINVAL;

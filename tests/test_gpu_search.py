@@ -367,3 +367,46 @@ def test_two_ply_cross_stream_after_destroyed_engine():
         assert torch.equal(torch.nan_to_num(Q1, 7.0), torch.nan_to_num(Q2, 7.0))
         assert torch.equal(b1, b2) and torch.equal(q1, q2)
         assert e.error() == 0
+
+
+def test_one_ply_selfplay_c2_batch():
+    """C2 at its BASELINE batch (B = 4,096 games, value MLP 198->40->1, Philox dice):
+    6 greedy 1-ply steps (one_ply then step).  At every step each choice is the FIRST
+    argmax of that lane's afterstate values (backgammon_env.py:207-216 features with the
+    mover's one-hot) and a legal move, and on a 64-lane sample the values of every
+    afterstate equal an oracle + torch fp32 composition (O.apply_move, O.features, the
+    torch value head) within 1e-5."""
+    import bgx
+    from bgx.policy import PolicyNet
+    from bgx.search import ValueHead, one_ply
+    torch.manual_seed(2)
+    net = PolicyNet(hidden_size=40).cuda()
+    vh = ValueHead(net)
+    B = 4096
+    eng = bgx.Engine(batch=B, max_moves=500, seed=123, dice="philox", auto_reset=True)
+    eng.reset(want_obs=False)
+    rng = np.random.RandomState(3)
+    for t in range(6):
+        best, bestv, vals = one_ply(eng, vh, want_values=True)
+        n = eng.n_moves()
+        rec, mv, _ = eng.lanes()
+        col = torch.arange(vals.shape[1], device="cuda")[None, :]
+        live = col < n[:, None].long()
+        vm = torch.where(live, vals, torch.full_like(vals, -float("inf")))
+        first = vm.argmax(dim=1).to(torch.int32)           # torch.argmax: the first maximum
+        has = n > 0
+        assert torch.equal(best[has], first[has]), t
+        assert bool((best[~has] == 0).all())
+        assert bool(torch.isfinite(vals[live]).all())
+        assert torch.equal(bestv[has], vm.max(dim=1).values[has])
+        recn, mvn, vn, nn = rec.cpu().numpy(), mv.cpu().numpy().view(np.uint64), vals.cpu().numpy(), n.cpu().numpy()
+        for i in rng.choice(B, 64, replace=False):
+            k = int(nn[i])
+            if k == 0:
+                continue
+            board, mover = recn[i, :52].view(np.int8), int(recn[i, 52])
+            feats = [O.features(O.apply_move(board, mover, int(mvn[i, a])), mover) for a in range(k)]
+            ref = _V(net, feats)
+            assert np.abs(vn[i, :k] - ref).max() < TOL, (t, i)
+        eng.step(best, want_obs=False, want_info=False)
+    assert eng.error() == 0
