@@ -389,6 +389,168 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
     return slow;
 }
 
+// nd_row without lane shuffles (round 5).  nd_row's chunk loop moves each chunk lane's
+// parent in with 16 ds_bpermute (a 6-step binary search for the parent, its child list,
+// prefix, node and meta): the counters put the light enumerator at 28 % of its wave time
+// stalled on LDS issue.  Here nothing crosses lanes through LDS:
+// * the parent of chunk position p is found from ballots: the "starters" (parents whose
+//   first child lies in this chunk) have start offsets k increasing with their lane, so
+//   the starters with k <= p are a prefix of them in lane order -- a bit-sliced compare of
+//   p against the six ballots of k's bits gives that set; its highest lane is the parent,
+//   and k itself is read back from the bit slices; positions before the first starter
+//   belong to the chunk's carry-in parent (the previous chunk's last);
+// * the parent's first sub-move (die, source) follows from its lane index and the
+//   wave-uniform per-die child lists, and its node, child list and meta are recomputed
+//   from the uniform root node (no bar, no bear-off in these rows: plain sub-moves).
+// Same leaves, in the same order, as nd_row (tests: BGX_2PLY_NDROW=1 runs nd_row).
+__device__ __forceinline__ void first_move_of(int x, const uint32_t (&K)[7], const int (&st)[8], int& d, int& a,
+                                              uint32_t& kd) {
+    d = 1;
+    #pragma unroll
+    for (int dd = 2; dd <= 6; ++dd) d = x >= st[dd] ? dd : d;
+    kd = K[1];
+    int kst = 0;
+    #pragma unroll
+    for (int dd = 2; dd <= 6; ++dd) { kd = d == dd ? K[dd] : kd; kst = d == dd ? st[dd] : kst; }
+    a = select_bit(kd, x - kst);
+}
+
+__device__ __forceinline__ uint32_t nd_row2(const S2& S, int row, const Node& s0, int q, uint32_t blocked,
+                                            KeySink& sink, unsigned long long& leaves) {
+    constexpr uint32_t kAllNd = 0x000B77BEu;        // the 15 non-doubles roll indices
+    const int off = (int)((s0.k3 >> 4) & 15u);
+    BG_CNT(1, 1);
+    if ((s0.k3 & 15u) != 0u || 15 - s0.n_home - off < 2) { BG_CNT(3, 1); return kAllNd; }
+    const int l = lane_id();
+    uint32_t K[7];
+    int st[8];
+    st[1] = 0;
+    K[0] = 0u;
+    #pragma unroll
+    for (int d = 1; d <= 6; ++d) {
+        K[d] = gen(s0, d, q, blocked).bits;
+        st[d + 1] = st[d] + __popc(K[d]);
+    }
+    const int n1 = st[7];
+    if (n1 > 64) { BG_CNT(3, 1); return kAllNd; }
+    // lane l: first sub-move (die dl, source al)
+    const bool act = l < n1;
+    int dl, al;
+    uint32_t kd;
+    first_move_of(act ? l : 0, K, st, dl, al, kd);
+    Node t1 = s0;
+    uint32_t Q[7];
+    Q[0] = 0u;
+    if (act) t1 = apply(s0, child(s0, Kids{kd, -1}, al, dl, q), q);
+    #pragma unroll
+    for (int e = 1; e <= 6; ++e) Q[e] = act && e != dl ? gen(t1, e, q, blocked).bits : 0u;
+    // roll (hi, lo) is fast iff its pass 1 (hi first) has a two-step
+    uint64_t M[7], N[7];
+    #pragma unroll
+    for (int d = 1; d <= 6; ++d) { M[d] = __ballot(act && dl == d); N[d] = __ballot(Q[d] != 0u); }
+    uint32_t slow = 0u;
+    #pragma unroll
+    for (int hi = 2; hi <= 6; ++hi)
+        #pragma unroll
+        for (int lo = 1; lo < hi; ++lo)
+            if (!(M[hi] & N[lo])) slow |= 1u << (roll_start(lo) + hi - lo);
+    const int sg = q == 0 ? 1 : -1;
+    const uint32_t root_occ = s0.occ, root_blot = s0.blot;
+    const uint32_t job0 = (uint32_t)row * 21u;
+    unsigned long long emitted = 0;
+    // a parent's two-steps with second die e (its child list for e, masked as nd_row)
+    auto kids_e = [&](const Node& t, int d, int a, int e) -> uint32_t {
+        const int hi = d > e ? d : e, lo = d > e ? e : d;
+        const int r = roll_start(lo) + hi - lo;
+        if (d == e || ((slow >> r) & 1u)) return 0u;
+        uint32_t c = gen(t, e, q, blocked).bits;
+        if (d < e) c &= 1u << (a + sg * d);
+        return c;
+    };
+    #pragma unroll 1
+    for (int e = 1; e <= 6; ++e) {
+        // the lane's first-level node again (cheaper than holding it across the loop)
+        const Node t1e = apply(s0, child(s0, Kids{kd, -1}, al, dl, q), q);
+        const uint32_t c = act ? kids_e(t1e, dl, al, e) : 0u;
+        const uint32_t cnt = (uint32_t)__popc(c);
+        uint32_t pre = 0, total = 0;
+        const uint64_t below = (1ull << l) - 1ull;
+        #pragma unroll
+        for (int b = 0; b < 5; ++b) {
+            const uint64_t m = __ballot((cnt >> b) & 1u);
+            pre += (uint32_t)__popcll(m & below) << b;
+            total += (uint32_t)__popcll(m) << b;
+        }
+        BG_CNT(5, (total + 63) / 64);
+        int carry_src = 0;
+        uint32_t carry_pre = 0;
+        for (uint32_t ch = 0; ch < total; ch += 64) {
+            // starters: parents whose first child position lies in [ch, ch + 64)
+            const bool starter = cnt > 0u && pre >= ch && pre < ch + 64u;
+            const uint32_t k = pre - ch;
+            const uint64_t B = __ballot(starter);
+            uint64_t kb[6];
+            #pragma unroll
+            for (int b = 0; b < 6; ++b) kb[b] = __ballot(starter && ((k >> b) & 1u));
+            // starters with k <= l (bit-sliced compare, most significant bit first)
+            uint64_t lt = 0ull, eq = B;
+            #pragma unroll
+            for (int b = 5; b >= 0; --b) {
+                const bool pb = (l >> b) & 1;
+                lt = pb ? lt | (eq & ~kb[b]) : lt;
+                eq = pb ? eq & kb[b] : eq & ~kb[b];
+            }
+            const uint64_t le = lt | eq;
+            int src = carry_src;
+            uint32_t psrc = carry_pre;
+            if (le) {
+                src = 63 - __clzll((long long)le);
+                uint32_t ks = 0u;
+                #pragma unroll
+                for (int b = 0; b < 6; ++b) ks |= (uint32_t)((kb[b] >> src) & 1ull) << b;
+                psrc = ch + ks;
+            }
+            carry_src = __builtin_amdgcn_readlane(src, 63);
+            carry_pre = (uint32_t)__builtin_amdgcn_readlane((int)psrc, 63);
+            const uint32_t pp = ch + (uint32_t)l;
+            const bool valid = pp < total;
+            Node leaf = s0;
+            bool emit = false;
+            int pr = 0;
+            if (valid) {
+                int pd, pa;
+                uint32_t pk;
+                first_move_of(src, K, st, pd, pa, pk);
+                const Node s1 = apply(s0, child(s0, Kids{pk, -1}, pa, pd, q), q);
+                const uint32_t qb = kids_e(s1, pd, pa, e);
+                const int hi = pd > e ? pd : e, lo = pd > e ? e : pd;
+                pr = roll_start(lo) + hi - lo;
+                const int cb = select_bit(qb, (int)(pp - psrc));
+                const Sub m = child(s1, Kids{qb, -1}, cb, e, q);
+                leaf = apply(s1, m, q);
+                if (pd > e) {               // pass 1: (pa, hi = pd) then (cb, lo = e)
+                    const int dst_a = pa + sg * pd;
+                    const bool chain = cb == dst_a, rev = m.dst == pa;
+                    emit = (!chain && !rev) ||
+                           nd_first_of(chain ? pa : cb, chain ? 1 : 2, e, pd, q, root_occ, root_blot, blocked);
+                } else {                    // pass 2: (pa, lo = pd) then its chain (cb, hi = e)
+                    emit = nd_first_of(pa, 3, pd, e, q, root_occ, root_blot, blocked);
+                }
+            }
+            const uint64_t em = __ballot(valid && emit);
+            sink.push_lanes_job(em, leaf, job0 + (uint32_t)pr, 2);
+            emitted += (unsigned long long)__popcll(em);
+        }
+    }
+    // every fast roll has a first pass-1 two-step (emitted): max length 2
+    const uint32_t fast = kAllNd & ~slow;
+    BG_CNT(4, __popc(slow));
+    BG_CNT(13, emitted);
+    if (l < 21 && ((fast >> l) & 1u) && !sink.lost) S.maxlen[job0 + (uint32_t)l] = 2;
+    if (!sink.lost) leaves += emitted;
+    return slow;
+}
+
 // The replier's node of row `row` (its 64-byte record, one byte per lane).
 __device__ __forceinline__ Node row_node(int bv, int& q, uint32_t& blocked) {
     q = rd(bv, 52);
@@ -423,7 +585,8 @@ __device__ __forceinline__ KeySink make_sink(const S2& S) {
 }
 
 // VARIANT 0: jobs (row, non-doubles roll) implicit, 1: (row, doubles roll)
-// implicit, 2: the explicit list, 3: as 0 with the row-level walk (nd_row) first.
+// implicit, 2: the explicit list, 3: as 0 with the row-level walk (nd_row) first,
+// 4: as 3 with nd_row2.
 template <int LOG, int MK, int VARIANT, int WPE = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_enum(S2 S) {
     __shared__ uint4 tab[1 << LOG];
@@ -431,7 +594,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     uint4* memo = MK >= 0 ? memo_ : nullptr;
     KeySink sink = make_sink(S);
     unsigned long long leaves = 0;
-    const int cap = VARIANT == 0 || VARIANT == 3 ? S.cap_light : S.cap_heavy;
+    const int cap = VARIANT == 0 || VARIANT >= 3 ? S.cap_light : S.cap_heavy;
     auto done = [&](int st, int job) {
         if (st == 1) {
             const int qo = LOG < 10 ? 0 : 1;
@@ -457,11 +620,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             int q;
             uint32_t blocked;
             const Node sq = row_node(bv, q, blocked);
-            if (VARIANT == 3) {
+            if (VARIANT >= 3) {
                 // the row-level walk; what it leaves (and a lost pool block: the
                 // whole row again) runs per job
                 BG_T0(t0);
-                uint32_t left = nd_row(S, row, sq, q, blocked, sink, leaves);
+                uint32_t left = VARIANT == 4 ? nd_row2(S, row, sq, q, blocked, sink, leaves)
+                                             : nd_row(S, row, sq, q, blocked, sink, leaves);
                 BG_T1(9, t0);
                 if (sink.lost) left = 0x000B77BEu;
                 BG_T0(t1);
@@ -1633,9 +1797,13 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
                                0, s, rowside, &ctr->rows, w1q, rowpart);
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    w1q, f16s + 4 + kKB * slices(NT) * 64 * 4, value_bias, factored ? rowpart : nullptr, nullptr};
-        // the non-doubles enumerator: the row-level walk held to 80 VGPRs (6 waves/SIMD,
-        // +1.2 % over its natural 91)
-        void (*klight)(S2) = k_enum<kLogLight, -1, 3, 6>;
+        // the non-doubles enumerator: the shuffle-free row walk (nd_row2) held to 96 VGPRs
+        // (5 waves/SIMD; at 80 it spills).  BGX_2PLY_NDROW=1 (tests, A/B): the round-4 row
+        // walk with lane shuffles (nd_row, 80 VGPRs: 6 waves/SIMD); =6: nd_row2 at 80 VGPRs
+        const char* ndr = getenv("BGX_2PLY_NDROW");
+        void (*klight)(S2) = k_enum<kLogLight, -1, 4, 5>;
+        if (ndr && ndr[0] == '1') klight = k_enum<kLogLight, -1, 3, 6>;
+        else if (ndr && ndr[0] == '6') klight = k_enum<kLogLight, -1, 4, 6>;
         const int g_light = persistent_grid(e, klight, 32);
         const int g_heavy = persistent_grid(e, kheavy, 32);
         const int g_list = persistent_grid(e, klist, 32);

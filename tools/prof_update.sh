@@ -30,4 +30,17 @@ span = int(last[-1]["End_Timestamp"]) - int(last[0]["Start_Timestamp"])
 print(f"last update: span {span/1e6:.3f} ms, GPU busy {busy/1e6:.3f} ms, kernels {len(last)}")
 for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
     print(f"{t/1e3:10.1f} us  x{c:3d}  {t/c/1e3:8.1f} us/call  {n}")
+# the largest idle gaps of the last update, with the kernels either side
+nm = lambda r: r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][-60:]
+gaps, end, prev = [], int(last[0]["End_Timestamp"]), last[0]
+for r in last[1:]:
+    s0 = int(r["Start_Timestamp"])
+    if s0 > end:
+        gaps.append((s0 - end, nm(prev), nm(r)))
+    if int(r["End_Timestamp"]) > end:
+        end, prev = int(r["End_Timestamp"]), r
+gaps.sort(reverse=True)
+print(f"idle gaps: {len(gaps)}, total {sum(g[0] for g in gaps)/1e6:.3f} ms; largest:")
+for g, a, b in gaps[:20]:
+    print(f"{g/1e3:9.1f} us  after {a}  before {b}")
 PY
