@@ -743,6 +743,14 @@ def main():
                      "rocprof_avg_us": prof_kernels,
                      "mean_legal_moves": mean_moves},
     }
+    # the same bytes chip-wide: every shard's env-step bytes over the whole step window
+    # (ms_per_step), while the per-shard figure above divides one shard's bytes by one
+    # shard's event window with the other shards' kernels sharing the GPU
+    ms_step = el * 1e3 / args.steps
+    chip = B * bytes_per_lane / (ms_step * 1e-3) / 1e9
+    line["roofline"]["chip_wide"] = {"achieved": chip, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": chip / HBM_PEAK_GBS, "algorithmic_bytes_per_step": B * bytes_per_lane,
+                                     "window_ms": ms_step, "note": "all shards' algorithmic env-step bytes / ms_per_step"}
     line["per_rank"] = [{"rank": k, "env_steps": r[0], "seconds": r[1]} for k, r in enumerate(per_rank)]
     if backend is not None:
         line["dist_backend"] = backend
@@ -828,6 +836,11 @@ def main():
                                                   (summ or {}).get("pmc_command") if prof_ok else None)
     if sq and sq.get("instructions_per_lane_step") and args.workload == "c3":
         line["roofline_issue"] = issue_roofline(sq, Bs, kern_ms, summ.get("pmc_command"))
+        # chip-wide: every lane-step of the whole GPU over ms_per_step (the per-CU scalar
+        # unit's real load; the object above prices one shard over its own event window)
+        cw = issue_roofline(sq, B, el * 1e3 / args.steps, summ.get("pmc_command"))
+        line["roofline_issue"]["chip_wide"] = {k: cw[k] for k in ("pipe", "achieved", "peak", "unit", "frac", "pipes")}
+        line["roofline_issue"]["chip_wide"]["window_ms"] = el * 1e3 / args.steps
     if args.two_ply_batches > 0:
         eng2 = engs[0] if S == 1 else bgx.Engine(batch=B, max_moves=500, seed=77 + rank, dice="philox",
                                                  auto_reset=True, device=dev)

@@ -392,6 +392,17 @@ int bgx_adam_step(int32_t n, float* const* params, float* const* grads, float* c
                   float* const* exp_avg_sq, float* const* steps, const int64_t* numels, double lr, double beta1,
                   double beta2, double eps, float* scale, int32_t* growth_tracker, float growth_factor,
                   float backoff_factor, int32_t growth_interval, int32_t* found, void* stream);
+/* The fused head's row plan for m rollout rows (replaces torch's argsort + bincount +
+ * cumsum in bgx/train.py ppo_row_plan, which are its CPU / reference form): a row's class
+ * is ceil(lim / 32) with lim = n_actions when its legal count (record bytes 60-61) is 0,
+ * else min(count, n_actions); perm_dev int32[m] = the rows ordered by class, stably (the
+ * order k_ppo_rows / k_ppo_gw2 read them in); plan_dev int32[33] = the k_ppo_gw2 task
+ * prefix per action tile (17) then the first row tile reaching each action tile (16);
+ * row_plan_dev int32[8] = the row-tile ranges of the bgx_ppo_rows variants.  Device
+ * only, no host sync; workspace_dev: bgx_ppo_plan_workspace(m) bytes. */
+int64_t bgx_ppo_plan_workspace(int32_t m);
+int bgx_ppo_plan(const uint8_t* records_dev, int32_t m, int32_t n_actions, int32_t* workspace_dev, int32_t* perm_dev,
+                 int32_t* plan_dev, int32_t* row_plan_dev, void* stream);
 int bgx_gather_rollout(const int32_t* perm_dev, int32_t n, const uint8_t* records_dev, const int32_t* actions_dev,
                        const float* old_logp_dev, const float* returns_dev, const float* adv_dev,
                        uint8_t* records_out, int32_t* actions_out, float* old_logp_out, float* returns_out,

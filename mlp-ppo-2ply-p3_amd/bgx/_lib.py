@@ -77,6 +77,8 @@ SIGNATURES = {
     "bgx_adam_step": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_double, _P, _P, ctypes.c_float, ctypes.c_float, _I32, _P, _P]),
     "bgx_gather_rollout": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "bgx_ppo_plan_workspace": (ctypes.c_int64, [_I32]),
+    "bgx_ppo_plan": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),
 }

@@ -346,6 +346,26 @@ FEAT_BIAS_COL = 198            # the ones column of the 208-wide rows: gW1[:, 19
 
 
 def ppo_row_plan(records: torch.Tensor, n_actions: int = 500):
+    """ppo_row_plan_torch on the GPU as three HIP launches (bgx_ppo_plan: a stable
+    counting sort by class plus the plan from the class totals), no host sync; the
+    torch form on the CPU."""
+    if not records.is_cuda:
+        return ppo_row_plan_torch(records, n_actions)
+    m = records.shape[0]
+    L = _lib.load()
+    dev = records.device
+    rec = records.contiguous()
+    ws = torch.empty(max(int(L.bgx_ppo_plan_workspace(m)) // 4, 1), dtype=torch.int32, device=dev)
+    perm = torch.empty(m, dtype=torch.int32, device=dev)
+    plan = torch.empty(33, dtype=torch.int32, device=dev)
+    row_plan = torch.empty(8, dtype=torch.int32, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    check(L.bgx_ppo_plan(p(rec), m, n_actions, p(ws), p(perm), p(plan), p(row_plan),
+                         ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "bgx_ppo_plan")
+    return perm, plan, row_plan
+
+
+def ppo_row_plan_torch(records: torch.Tensor, n_actions: int = 500):
     """Row order and work plan of bgx_ppo_rows / bgx_ppo_gw2 for one chunk of
     rollout rows (computed once per update; the records do not change across
     epochs).  A row needs the 32-action tiles holding its legal columns

@@ -827,6 +827,120 @@ __global__ __launch_bounds__(256) void k_gather_rollout(const int32_t* __restric
     else adv_o[i] = adv[src];
 }
 
+// ---- the fused head's row plan on the device (bgx_ppo_plan; round 5).  A row's class
+// is the number of 32-action tiles it needs: ceil(lim / 32), lim = n_actions for a row
+// with no legal move, else min(count, n_actions) (the count from record bytes 60-61).
+// The rows are ordered by class, stably (a counting sort: per-block class counts, one
+// block scanning them per class, then each row's rank from ballots), and the plan of
+// k_ppo_gw2 / the bgx_ppo_rows variants follows from the 17 class totals.  Replaces
+// torch's argsort + bincount (a host sync: bincount sizes its output from the data) +
+// cumsum and a dozen small launches of round 4's ppo_row_plan.
+constexpr int kPlanCls = 17;                 // classes 0..16 (0 never occurs)
+constexpr int kPlanRows = 1024;              // rows per counting block
+
+__device__ __forceinline__ int plan_class(const uint8_t* rec, int64_t i, int n_actions) {
+    const int cnt = (int)rec[i * 64 + 60] | ((int)rec[i * 64 + 61] << 8);
+    const int lim = cnt == 0 ? n_actions : (cnt < n_actions ? cnt : n_actions);
+    return (lim + 31) >> 5;
+}
+
+// per-wave class counts of this block's rows (LDS wc[16][17]); returns the row's class
+// (0 past the end) and its rank among the wave's rows of that class
+__device__ __forceinline__ int plan_wave_counts(const uint8_t* rec, int m, int n_actions, int (*wc)[kPlanCls],
+                                                int& rank) {
+    const int64_t i = (int64_t)blockIdx.x * kPlanRows + threadIdx.x;
+    const int c = i < m ? plan_class(rec, i, n_actions) : 0;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const uint64_t below = (1ull << l) - 1ull;
+    rank = 0;
+    #pragma unroll
+    for (int k = 1; k < kPlanCls; ++k) {
+        const uint64_t b = __ballot(c == k);
+        if (c == k) rank = __popcll(b & below);
+        if (l == 0) wc[w][k] = __popcll(b);
+    }
+    if (l == 0) wc[w][0] = 0;
+    __syncthreads();
+    return c;
+}
+
+__global__ __launch_bounds__(kPlanRows) void k_plan_count(const uint8_t* __restrict__ rec, int m, int n_actions,
+                                                          int32_t* __restrict__ bcnt) {
+    __shared__ int wc[kPlanRows / 64][kPlanCls];
+    int rank;
+    (void)plan_wave_counts(rec, m, n_actions, wc, rank);
+    if (threadIdx.x < kPlanCls) {
+        int t = 0;
+        #pragma unroll
+        for (int w = 0; w < kPlanRows / 64; ++w) t += wc[w][threadIdx.x];
+        bcnt[(size_t)blockIdx.x * kPlanCls + threadIdx.x] = t;
+    }
+}
+
+// one workgroup, wave k - 1 scanning class k over the blocks: boff[b][k] = the sorted
+// position of block b's first class-k row; then the plan from the class totals
+__global__ __launch_bounds__(1024) void k_plan_scan(const int32_t* __restrict__ bcnt, int nb, int m,
+                                                    int32_t* __restrict__ boff, int32_t* __restrict__ plan,
+                                                    int32_t* __restrict__ row_plan) {
+    __shared__ int tot[kPlanCls];
+    __shared__ int base[kPlanCls];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, k = w + 1;
+    int run = 0;
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + l;
+        const int v = b < nb ? bcnt[(size_t)b * kPlanCls + k] : 0;
+        int x = v;                                       // inclusive scan over the 64 lanes
+        #pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (l >= o) x += y;
+        }
+        if (b < nb) boff[(size_t)b * kPlanCls + k] = run + x - v;
+        run += __shfl(x, 63);
+    }
+    if (l == 0) tot[k] = run;
+    if (threadIdx.x == 0) tot[0] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        int cum[kPlanCls];
+        for (int c = 0; c < kPlanCls; ++c) { base[c] = acc; acc += tot[c]; cum[c] = acc; }
+        // ppo_row_plan (bgx/train.py): start[o] = first row tile reaching action tile o
+        // (the value column's tile 15: every row); tasks of kTS row tiles per action tile
+        const int ntiles = (m + 31) / 32;
+        int pre = 0;
+        for (int o = 0; o < 16; ++o) {
+            const int st = o == 15 ? 0 : cum[o] / 32;
+            plan[17 + o] = st;
+            plan[o] = pre;
+            pre += (ntiles - st + kTS - 1) / kTS;
+        }
+        plan[16] = pre;
+        int e[3];
+        const int ks[3] = {1, 2, 4};
+        for (int j = 0; j < 3; ++j) e[j] = cum[ks[j]] >= m ? ntiles : cum[ks[j]] / 32;
+        row_plan[0] = 0; row_plan[1] = e[0]; row_plan[2] = e[0]; row_plan[3] = e[1];
+        row_plan[4] = e[1]; row_plan[5] = e[2]; row_plan[6] = e[2]; row_plan[7] = ntiles;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += 1024)
+        #pragma unroll
+        for (int c = 1; c < kPlanCls; ++c) boff[(size_t)b * kPlanCls + c] += base[c];
+}
+
+__global__ __launch_bounds__(kPlanRows) void k_plan_scatter(const uint8_t* __restrict__ rec, int m, int n_actions,
+                                                            const int32_t* __restrict__ boff,
+                                                            int32_t* __restrict__ perm) {
+    __shared__ int wc[kPlanRows / 64][kPlanCls];
+    int rank;
+    const int c = plan_wave_counts(rec, m, n_actions, wc, rank);
+    const int64_t i = (int64_t)blockIdx.x * kPlanRows + threadIdx.x;
+    if (i >= m) return;
+    int off = boff[(size_t)blockIdx.x * kPlanCls + c] + rank;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += wc[w][c];
+    perm[off] = (int32_t)i;
+}
+
 // ---- the optimizer step (bgx_adam_step): torch.optim.Adam(fused=True) driven by
 // GradScaler.step + update, as three launches over the flat element range of every
 // tensor instead of torch's per-tensor multi-tensor chunks (a 90 k-parameter net ran
@@ -1054,6 +1168,28 @@ extern "C" int bgx_gather_rollout(const int32_t* perm, int32_t n, const uint8_t*
     hipLaunchKernelGGL(k_gather_rollout, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        perm, n, (const uint4*)records, actions, old_logp, returns, adv, (uint4*)records_out,
                        actions_out, old_logp_out, returns_out, adv_out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
+extern "C" int64_t bgx_ppo_plan_workspace(int32_t m) {
+    if (m < 0) return BGX_EINVAL;
+    const int64_t nb = ((int64_t)m + kPlanRows - 1) / kPlanRows;
+    return 2 * nb * kPlanCls * 4;
+}
+
+extern "C" int bgx_ppo_plan(const uint8_t* records, int32_t m, int32_t n_actions, int32_t* workspace, int32_t* perm,
+                            int32_t* plan, int32_t* row_plan, void* stream) {
+    if (m < 0 || n_actions <= 0 || n_actions > kNT * 32 - 1 || (m > 0 && (!records || !workspace || !perm)) ||
+        !plan || !row_plan)
+        return BGX_EINVAL;
+    const int nb = (m + kPlanRows - 1) / kPlanRows;
+    hipStream_t s = (hipStream_t)stream;
+    int32_t* bcnt = workspace;
+    int32_t* boff = workspace + (size_t)nb * kPlanCls;
+    if (nb > 0) hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, bcnt);
+    hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, bcnt, nb, m, boff, plan, row_plan);
+    if (nb > 0) hipLaunchKernelGGL(k_plan_scatter, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, boff, perm);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }

@@ -199,3 +199,34 @@ def test_gather_rollout_matches_torch_indexing():
     pl = perm.long()
     for a, b in zip(got, (recs[pl], acts[pl], old[pl], R[pl], adv[pl])):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("m", [1, 31, 1024, 4097, 3 * 65536 + 77, (1 << 20) + 5])
+def test_device_row_plan_matches_torch(m):
+    """bgx_ppo_plan (stable counting sort by action-tile class + the k_ppo_gw2 / rows
+    plan from the class totals, no host sync) equals the torch form it replaces
+    (argsort stable + bincount + cumsum, ppo_row_plan_torch) exactly: legal counts 0
+    (all 16 tiles), 1..500 and above n_actions, at sizes around the 1,024-row blocks."""
+    from bgx.train import ppo_row_plan, ppo_row_plan_torch
+    g = torch.Generator(device="cpu").manual_seed(m)
+    recs = torch.randint(0, 256, (m, 64), dtype=torch.uint8, generator=g)
+    kind = torch.randint(0, 10, (m,), generator=g)
+    cnt = torch.where(kind == 0, torch.zeros(m, dtype=torch.int64),
+                      torch.where(kind == 1, torch.randint(501, 2000, (m,), generator=g),
+                                  torch.randint(1, 60, (m,), generator=g)))
+    cnt = torch.where(kind == 2, torch.randint(60, 501, (m,), generator=g), cnt)
+    recs[:, 60] = (cnt & 255).to(torch.uint8)
+    recs[:, 61] = (cnt >> 8).to(torch.uint8)
+    recs = recs.cuda()
+    p1, pl1, rp1 = ppo_row_plan(recs)
+    p2, pl2, rp2 = ppo_row_plan_torch(recs)
+    assert torch.equal(p1, p2)
+    assert torch.equal(pl1, pl2)
+    assert torch.equal(rp1, rp2)
+
+
+def test_device_row_plan_on_rollout():
+    from bgx.train import ppo_row_plan, ppo_row_plan_torch
+    recs = _setup(seed=5, batch=2048, horizon=6)[0]
+    for a, b in zip(ppo_row_plan(recs), ppo_row_plan_torch(recs)):
+        assert torch.equal(a, b)
