@@ -393,12 +393,7 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
 // parent in with 16 ds_bpermute (a 6-step binary search for the parent, its child list,
 // prefix, node and meta): the counters put the light enumerator at 28 % of its wave time
 // stalled on LDS issue.  Here nothing crosses lanes through LDS:
-// * the parent of chunk position p is found from ballots: the "starters" (parents whose
-//   first child lies in this chunk) have start offsets k increasing with their lane, so
-//   the starters with k <= p are a prefix of them in lane order -- a bit-sliced compare of
-//   p against the six ballots of k's bits gives that set; its highest lane is the parent,
-//   and k itself is read back from the bit slices; positions before the first starter
-//   belong to the chunk's carry-in parent (the previous chunk's last);
+// * the parent of chunk position p is found from ballots (chunk_parent, bg_core.h);
 // * the parent's first sub-move (die, source) follows from its lane index and the
 //   wave-uniform per-die child lists, and its node, child list and meta are recomputed
 //   from the uniform root node (no bar, no bear-off in these rows: plain sub-moves).
@@ -485,33 +480,8 @@ __device__ __forceinline__ uint32_t nd_row2(const S2& S, int row, const Node& s0
         int carry_src = 0;
         uint32_t carry_pre = 0;
         for (uint32_t ch = 0; ch < total; ch += 64) {
-            // starters: parents whose first child position lies in [ch, ch + 64)
-            const bool starter = cnt > 0u && pre >= ch && pre < ch + 64u;
-            const uint32_t k = pre - ch;
-            const uint64_t B = __ballot(starter);
-            uint64_t kb[6];
-            #pragma unroll
-            for (int b = 0; b < 6; ++b) kb[b] = __ballot(starter && ((k >> b) & 1u));
-            // starters with k <= l (bit-sliced compare, most significant bit first)
-            uint64_t lt = 0ull, eq = B;
-            #pragma unroll
-            for (int b = 5; b >= 0; --b) {
-                const bool pb = (l >> b) & 1;
-                lt = pb ? lt | (eq & ~kb[b]) : lt;
-                eq = pb ? eq & kb[b] : eq & ~kb[b];
-            }
-            const uint64_t le = lt | eq;
-            int src = carry_src;
-            uint32_t psrc = carry_pre;
-            if (le) {
-                src = 63 - __clzll((long long)le);
-                uint32_t ks = 0u;
-                #pragma unroll
-                for (int b = 0; b < 6; ++b) ks |= (uint32_t)((kb[b] >> src) & 1ull) << b;
-                psrc = ch + ks;
-            }
-            carry_src = __builtin_amdgcn_readlane(src, 63);
-            carry_pre = (uint32_t)__builtin_amdgcn_readlane((int)psrc, 63);
+            uint32_t psrc;
+            const int src = chunk_parent(cnt, pre, ch, carry_src, carry_pre, &psrc);
             const uint32_t pp = ch + (uint32_t)l;
             const bool valid = pp < total;
             Node leaf = s0;
@@ -832,14 +802,11 @@ __device__ __forceinline__ uint32_t f16_pair(uint32_t ab, float s0, float s1) {
 // f16 pairs [u_k(a), u_k(b)], k = 0..3: n>=1, n>=2, n>=3, (n-3)/2 if n>=3.
 // t = (1024 + a, 1024 + b) in f16 (unit spacing there, so every step is exact):
 // u_k = clamp01(t - 1024 - k) for k < 3, u_3 = max(t/2 - 513.5, 0).  Written with
-// builtins: hipcc folds min(max(x, 0), 1) into the VOP3P clamp bit, so this is the same
-// five instructions (3 v_pk_add_f16 clamp, v_pk_fma_f16, v_pk_max_f16) as the round-3/4
-// inline-asm block, but visible to the hazard recognizer.  That block was the cause of the
-// two-tiles-in-flight fault: with accumulators in VGPRs an MFMA may
-// write D to other registers than its C, and the allocator then reused a C register, still
-// being read by the in-flight MFMA (an XDL SrcC read runs over its passes), as an asm output:
-// a VALU write into an in-flight SrcC (WAR) that hipcc pads for its own VALU code but cannot
-// see inside an asm string.
+// builtins (round 5): hipcc folds min(max(x, 0), 1) into the VOP3P clamp bit, so this is
+// the same five instructions (3 v_pk_add_f16 clamp, v_pk_fma_f16, v_pk_max_f16) as the
+// round-3/4 inline-asm block, and the hazard recognizer now sees every one of them (the
+// asm string hid them; it was not the cause of the two-tiles-in-flight fault, which the
+// builtin form shows as well: eval_tile_wide).
 __device__ __forceinline__ h16x2 clamp01h(h16x2 x) {
     return __builtin_elementwise_min(__builtin_elementwise_max(x, (h16x2){0, 0}), (h16x2){1, 1});
 }
@@ -905,45 +872,53 @@ __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0
 // asm would hide the MFMA-result read from the hazard recognizer, which must pad it)
 __device__ __forceinline__ float relu_raw(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
-// Wide tiles (H > 64): both 32-column leaf tiles in flight, sharing every weight fragment
-// (128 accumulator VGPRs at H = 128).
+// Wide tiles (H > 64), one leaf tile of 32 columns at a time.  Two leaf tiles in flight
+// (sharing each weight fragment, 128 accumulator VGPRs at H = 128; -DBGX_WIDE_PAIR builds
+// that form for experiments) give wrong values in columns 16-31 of the second tile for a
+// few leaves, varying with the build's instruction layout -- with the feature units as
+// inline asm (rounds 3-4) and as builtins (round 5) alike, with no EXEC-masked MFMA, no
+// MFMA whose D differs from its C, and every MFMA-result read >= 12 wait states after its
+// producer in the ISA.  One tile at a time is exact on every leaf
+// (test_two_ply_every_leaf_vs_fp64: all 534 k leaves of a 48-root batch against fp64).
 template <int NT>
-__device__ __forceinline__ void eval_leaves_wide(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z,
-                                                 float bias, float (&v)[2]) {
+__device__ __forceinline__ float eval_tile_wide(const uint4* wq, const float* wvs, const Leaf& L, int z, float bias) {
     constexpr int NW = slices(NT) / 2;
     const int l = lane_id(), h = l >> 5;
-    f32x16 x[2][NW];
+    f32x16 x[NW];
     #pragma unroll
     for (int kb = 0; kb < kKB; ++kb) {
-        const f16x8 f[2] = {feat16(L[0], kb, h), feat16(L[1], kb, h)};
+        const f16x8 f = feat16(L, kb, h);
         #pragma unroll
         for (int t = 0; t < NW; ++t) {
             const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 0) * 64 + l + z]);
             const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * NW + t) * 2 + 1) * 64 + l + z]);
-            #pragma unroll
-            for (int n = 0; n < 2; ++n) {
-                x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f[n], kb == 0 ? (f32x16){} : x[n][t], 0, 0, 0);
-                x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f[n], x[n][t], 0, 0, 0);
-            }
+            x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f, kb == 0 ? (f32x16){} : x[t], 0, 0, 0);
+            x[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f, x[t], 0, 0, 0);
         }
     }
     // value head: relu times the head weights, 4 registers' weights per ds_read_b128
-    float a[2] = {0.0f, 0.0f};
+    float a = 0.0f;
     #pragma unroll
     for (int t = 0; t < NW; ++t)
         #pragma unroll
         for (int r4 = 0; r4 < 4; ++r4) {
             const float4 w = reinterpret_cast<const float4*>(wvs)[(t * 4 + r4) * 64 + l + z];
-            #pragma unroll
-            for (int n = 0; n < 2; ++n) {
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 0]), w.x, a[n]);
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 1]), w.y, a[n]);
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 2]), w.z, a[n]);
-                a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 3]), w.w, a[n]);
-            }
+            a = fmaf(relu_raw(x[t][4 * r4 + 0]), w.x, a);
+            a = fmaf(relu_raw(x[t][4 * r4 + 1]), w.y, a);
+            a = fmaf(relu_raw(x[t][4 * r4 + 2]), w.z, a);
+            a = fmaf(relu_raw(x[t][4 * r4 + 3]), w.w, a);
         }
-    #pragma unroll
-    for (int n = 0; n < 2; ++n) v[n] = a[n] + __shfl_xor(a[n], 32) + bias;
+    return a + __shfl_xor(a, 32) + bias;
+}
+
+template <int NT>
+__device__ __forceinline__ void eval_leaves_wide(const uint4* wq, const float* wvs, const Leaf (&L)[2], int z,
+                                                 float bias, float (&v)[2]) {
+    v[0] = eval_tile_wide<NT>(wq, wvs, L[0], z, bias);
+    __builtin_amdgcn_sched_barrier(0);              // the tiles stay apart (not interleaved)
+    int z1 = z;                                     // opaque: the second tile re-reads its fragments
+    __asm__ volatile("" : "+s"(z1));
+    v[1] = eval_tile_wide<NT>(wq, wvs, L[1], z1, bias);
 }
 
 template <int NT>
@@ -1132,6 +1107,11 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
         for (int n = 0; n < NN; ++n) f[n] = hit_delta(L[n].hits, k6, h);
         block(6 * P + k6, f, false);
     }
+#ifdef BGX_EVAL_PAD
+    __builtin_amdgcn_sched_barrier(0);
+    __asm__ volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     if constexpr (kLate)
     #pragma unroll
     for (int n = 0; n < NN; ++n)
@@ -1299,7 +1279,18 @@ void k_eval(EvalArgs E) {
                 float w[2];
                 int zq = z;                               // opaque per pass: no LDS read hoisted out
                 __asm__ volatile("" : "+s"(zq));
-                eval_leaves_fact<NT, 2>(wq, wvs, F, zq, E.bv, E.rowpart, qq, w);
+#ifndef BGX_WIDE_PAIR
+                if constexpr (wide_tiles(NT)) {         // one leaf tile at a time (eval_tile_wide)
+                    eval_leaves_fact<NT, 1>(wq, wvs, &F[0], zq, E.bv, E.rowpart, qq, &w[0]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    int zr = zq;
+                    __asm__ volatile("" : "+s"(zr));
+                    eval_leaves_fact<NT, 1>(wq, wvs, &F[1], zr, E.bv, E.rowpart, qq, &w[1]);
+                } else
+#endif
+                {
+                    eval_leaves_fact<NT, 2>(wq, wvs, F, zq, E.bv, E.rowpart, qq, w);
+                }
                 #pragma unroll
                 for (int n = 0; n < 2; ++n) v[n] = L[n].q == qq ? w[n] : v[n];
             }
