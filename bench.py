@@ -49,9 +49,10 @@ def parse():
                     help="also time full PPO iterations (T rollout steps + update); 0 = skip")
     ap.add_argument("--two-ply-batches", type=int, default=2,
                     help="C4: timed 2-ply expectimax passes over all B root positions (0 = skip)")
-    ap.add_argument("--c4-shards", type=int, default=2,
+    ap.add_argument("--c4-shards", type=int, default=4,
                     help="C4 (H = 40): the B roots as S engines on S streams and host threads, so one shard's "
-                         "reply enumeration runs beside another's evaluation")
+                         "reply enumeration runs beside another's evaluation (S=1 1.61 M, S=4 1.82 M, S=8 1.82 M "
+                         "root decisions/s; DESIGN.md §8 Round 5)")
     ap.add_argument("--c2-steps", type=int, default=50,
                     help="C2: timed greedy 1-ply self-play steps at B=4096 (0 = skip)")
     ap.add_argument("--c2-shards", type=int, default=4,

@@ -339,41 +339,6 @@ __device__ __forceinline__ int parent_of(uint32_t pp, uint32_t incl) {
     return i < 64 ? i : 63;
 }
 
-// The flat chunk's parent lookup without lane shuffles (round 5): positions
-// [ch, ch + 64) of a flat child list, lane p holding position ch + p; parent lanes hold
-// cnt children starting at position pre (pre non-decreasing over the lanes).  The
-// "starters" (cnt > 0, first child inside the chunk) have offsets k = pre - ch that
-// increase with their lane, so the starters with k <= p are a prefix of them in lane
-// order: a bit-sliced compare of p against the six ballots of k's bits gives that set,
-// its highest lane is p's parent, whose first position is one shuffle of pre away.
-// Positions before the first starter belong to the previous chunk's last parent
-// (carry_src / carry_pre, wave-uniform, updated here).  Returns p's parent lane and its
-// first position in *psrc: 7 ballots, one ds_bpermute and ~50 VALU instead of
-// parent_of's 6 dependent ds_bpermute plus the shuffles that bring the parent's state over.
-__device__ __forceinline__ int chunk_parent(uint32_t cnt, uint32_t pre, uint32_t ch, int& carry_src,
-                                            uint32_t& carry_pre, uint32_t* psrc) {
-    const int l = threadIdx.x & 63;
-    const bool starter = cnt > 0u && pre >= ch && pre < ch + 64u;
-    const uint32_t k = pre - ch;
-    uint64_t lt = 0ull, eq = __ballot(starter);
-    #pragma unroll
-    for (int b = 5; b >= 0; --b) {            // one ballot live at a time (SGPR pressure)
-        const uint64_t kb = __ballot(starter && ((k >> b) & 1u));
-        const bool pb = (l >> b) & 1;
-        lt = pb ? lt | (eq & ~kb) : lt;
-        eq = pb ? eq & kb : eq & ~kb;
-    }
-    const uint64_t le = lt | eq;
-    const int src = le ? 63 - __clzll((long long)le) : carry_src;
-    // the parent's first position: one shuffle (its lane's pre), or the carry
-    const uint32_t ps_sh = (uint32_t)__shfl((int)pre, src);
-    const uint32_t ps = le ? ps_sh : carry_pre;
-    carry_src = __builtin_amdgcn_readlane(src, 63);
-    carry_pre = (uint32_t)__builtin_amdgcn_readlane((int)ps, 63);
-    *psrc = ps;
-    return src;
-}
-
 __device__ __forceinline__ int lane_rank(uint64_t m) {          // set bits of m below this lane
     const int lane = threadIdx.x & 63;
     return __popcll(m & ((1ull << lane) - 1ull));
@@ -665,69 +630,6 @@ struct Gen {
         }
     }
 
-    // flat_leaves for nd_both's two-step batch without lane shuffles (round 5): a chunk
-    // lane's parent comes from chunk_parent, and the parent's state -- its first sub-move
-    // (child bit = lane & 31 of the first level of pass 1 (lanes 0-31, die hi) or pass 2
-    // (lanes 32-63, die lo)), node, child list and encoding -- is recomputed from the
-    // wave-uniform root instead of shuffled over.  both: nd_both's single batch of both
-    // passes (pass-2 parents keep only their chain child); else the sequential form's
-    // pass-2 batch.  The same entries, in the same order, as flat_leaves.
-    __device__ __forceinline__ void flat_leaves_nd(uint64_t parents, uint32_t q, const Node& s0, const Kids& kh,
-                                                   const Kids& kl, int hi, int lo, bool both) {
-        const int l = threadIdx.x & 63;
-        const bool par = (parents >> l) & 1ull;
-        const uint32_t cnt = par ? (uint32_t)__popc(q) : 0u;         // <= 25
-        uint32_t pre = 0, total = 0;
-        const uint64_t below = (1ull << l) - 1ull;
-        #pragma unroll
-        for (int b = 0; b < 5; ++b) {
-            const uint64_t m = __ballot((cnt >> b) & 1u);
-            pre += (uint32_t)__popcll(m & below) << b;
-            total += (uint32_t)__popcll(m) << b;
-        }
-        BG_CNT(6, 1);
-        BG_CNT(7, total);
-        int carry_src = 0;
-        uint32_t carry_pre = 0u;
-        for (uint32_t c = 0; c < total; c += 64) {
-            const uint32_t pp = c + (uint32_t)l;
-            const bool valid = pp < total;
-            uint32_t psrc;
-            const int src = chunk_parent(cnt, pre, c, carry_src, carry_pre, &psrc);
-            Node leaf;
-            uint64_t enc = 0;
-            uint32_t slot = 0;
-            bool found = true, pure = false;
-            if (valid) {
-                const bool up = src >= 32;
-                const int bit = src & 31, da = up ? lo : hi, db = up ? hi : lo;
-                const Kids k1{up ? kl.bits : kh.bits, up ? kl.extra : kh.extra};
-                const Sub m1 = child(s0, k1, bit, da, pl);
-                const Node s = apply(s0, m1, pl);
-                const Kids k2 = gen(s, db, pl, blocked);
-                uint32_t qb = k2.bits;
-                if (both && up && bit < 24) qb &= (1u << 31) | (1u << (pl == 0 ? bit + da : bit - da));
-                const int cb = select_bit(qb, (int)(pp - psrc));
-                const Sub m = child(s, k2, cb, db, pl);
-                leaf = apply(s, m, pl);
-                enc = Sink::kEnc ? (uint64_t)m1.enc | ((uint64_t)m.enc << 16) : 0ull;
-                if (both && src < 24 && cb < 24) {
-                    const int dst_a = pl == 0 ? src + hi : src - hi;
-                    pure = cb != dst_a && m.dst != src;
-                    if (nd_free && !pure) pure = nd_first(cb == dst_a ? src : cb, cb == dst_a ? 1 : 2, lo, hi);
-                } else if (nd_free) {
-                    pure = nd_first(src - 32, 3, lo, hi);      // pass 2: a chain (no specials here)
-                }
-                pure = pure || pure_walk;
-                if (!pure && !nd_free)
-                    found = probe_lane<LOG_SLOTS>(tab, (uint32_t)leaf.lo, (uint32_t)(leaf.lo >> 32), leaf.hi, leaf.k3, slot);
-            }
-            if (nd_free) { commit(0ull, leaf, enc, slot, 2, __ballot(valid && pure)); continue; }
-            commit<true>(__ballot(valid && !pure && !found), leaf, enc, slot, 2, __ballot(valid && pure));
-            if (ovf) return;
-        }
-    }
-
     // handle_non_doubles (handle_moves.py:109-200) for both dice orders of
     // get_all_possible_moves (get_all_moves.py:33-53) at once: lanes 0-31 hold the
     // first level of pass 1 (hi then lo; lane = child bit), lanes 32-63 that of
@@ -787,22 +689,14 @@ struct Gen {
             nd_free = (s0.k3 & 15u) == 0u && 15 - s0.n_home - (int)((s0.k3 >> 4) & 15u) >= 2;
             if (nd_free) { root_occ = s0.occ; root_blot = s0.blot; }
             else need_table();
-#ifdef BGX_ND_SHFL
             flat_leaves(par, t1, q2, x2, (uint64_t)e1, lo, 16, 2, hi);
-#else
-            flat_leaves_nd(par, q2, s0, kh, kl, hi, lo, true);
-#endif
             nd_free = false;
             return;
         }
         need_table();
         batch(a1 && !up, t1, (uint64_t)e1, 1);                  // pass 1: singles
         if (ovf || (n_unique == 1 && cur_max == 1)) return;     // :41-53
-#ifdef BGX_ND_SHFL
         if (two) flat_leaves(two, t1, q2, x2, (uint64_t)e1, hi, 16, 2);
-#else
-        if (two) flat_leaves_nd(two, q2, s0, kh, kl, hi, lo, false);
-#endif
         else batch(a1 && up, t1, (uint64_t)e1, 1);
     }
 

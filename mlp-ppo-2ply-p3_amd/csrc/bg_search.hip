@@ -45,9 +45,26 @@ using namespace bg;
 
 namespace {
 
+// Work counters of the 2-ply enumerators (experiments, -DBGX_COUNTERS; tools/enum_counters.py):
+// this file's own set, apart from bg_core.h's move-generator counters
+#ifdef BGX_COUNTERS
+__device__ unsigned long long g_scnt[16];
+#define SC_CNT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_scnt[i], (unsigned long long)(v)); } while (0)
+#define SC_T0(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define SC_T1(i, t) SC_CNT(i, __builtin_amdgcn_s_memtime() - t)
+#else
+#define SC_CNT(i, v) do { } while (0)
+#define SC_T0(t) do { } while (0)
+#define SC_T1(i, t) do { } while (0)
+#endif
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+#ifdef BGX_PAIR_1WAVE
+constexpr int kEvalWideWaves = 4, kEvalNarrowWaves = 4;   // experiment: one wave per SIMD at H = 128
+#else
 constexpr int kEvalWideWaves = 8, kEvalNarrowWaves = 4;   // waves per LDS-weight evaluator workgroup
+#endif   // waves per LDS-weight evaluator workgroup
 constexpr int kKB = 13;            // 208 / 16 k-steps of v_mfma_f32_32x32x16_f16
 constexpr int kSlowQueue = 1 << 20;
 constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
@@ -154,6 +171,7 @@ struct S2 {
     int32_t* err;
     int cap_light, cap_heavy, cap_mid;   // unique-entry capacity of the LDS tables (tests shrink them)
     int memo_mask, memo_share;           // revisit memo at depth 2 (bit 0) / 3 (bit 1); in-table share /8
+    int bar_rows;                        // nd_row_bar on (tests turn it off: BGX_2PLY_BARROW=0)
 };
 
 __device__ __forceinline__ unsigned long long bcast64(unsigned long long v) {
@@ -268,6 +286,100 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, int r, int q, cons
     return 0;
 }
 
+// All 15 non-doubles rolls of a row whose replier has checkers on the bar (round 5; the
+// counters put 44 % of C4's rows here, and the light enumerator spent most of its wave time
+// in their 15 per-job walks, each clearing and probing a dedup table).  The first sub-move
+// of either die order is the bar entry, and no bear-off can follow (an entered checker
+// stands outside its home), so nd_both's paths (handle_non_doubles + the skip rule,
+// get_all_moves.py:33-53) reduce to closed cases, table-free:
+// * two or more on the bar: both entries open -> one leaf (both orders give the same
+//   afterstate), length 2; only one open -> that entry, length 1 (pass 1's single ends the
+//   walk, or pass 1 is empty and pass 2 has it); none -> no reply (the leaf is a itself);
+// * one on the bar, e(d) the entry point of die d: with e(hi) open and a lo-move after
+//   it, family A = enter hi then any lo-move (the entered checker included) and family B =
+//   enter lo then any hi-move, length 2.  Within a family the sources differ, so the
+//   states do; across them the count changes {+e(hi), -c, +(c+lo)} and {+e(lo), -c',
+//   +(c'+hi)} agree only for the chain through the entry points (c = e(hi), c' = e(lo):
+//   both end at e(hi) + lo = e(lo) + hi), and then the states are equal iff neither entry
+//   point held a blot (the hit sets differ otherwise): the set is A plus B without that
+//   chain when it repeats A's.  e(hi) open but no lo-move after it: pass 1's single entry
+//   ends the walk (the skip rule), length 1.  e(hi) blocked: family B (length 2), or the
+//   lo entry alone (length 1), or no reply.
+// Lane l < 24: A's child from point l; lane 32 + l: B's.
+__device__ __forceinline__ uint32_t nd_row_bar(const S2& S, int row, const Node& s0, int q, uint32_t blocked,
+                                               KeySink& sink, unsigned long long& leaves) {
+    const int l = lane_id();
+    const int bar = (int)(s0.k3 & 15u);
+    const uint32_t job0 = (uint32_t)row * 21u;
+    uint32_t open = 0u;                              // dice whose entry point is open
+    #pragma unroll
+    for (int d = 1; d <= 6; ++d) open |= ((blocked >> entry_point(q, d)) & 1u) ? 0u : 1u << d;
+    const Kids kbar{1u << 31, kBar};
+    unsigned long long emitted = 0;
+    if (bar >= 2) {
+        // lane k < 15: the k-th non-doubles roll; one leaf per roll
+        int lo = 1, hi = 2;
+        const int r = l < 15 ? nd_roll(l) : 0;
+        if (l < 15) roll_dice(r, lo, hi);
+        const bool oh = (open >> hi) & 1u, ol = (open >> lo) & 1u;
+        Node leaf = s0;
+        if (oh) leaf = apply(leaf, child(leaf, kbar, 31, hi, q), q);
+        if (ol) leaf = apply(leaf, child(leaf, kbar, 31, lo, q), q);
+        const int len = (int)oh + (int)ol;
+        const bool on = l < 15;
+        #pragma unroll
+        for (int n = 0; n <= 2; ++n) {              // the pool tag carries the length
+            const uint64_t em = __ballot(on && len == n);
+            if (em) sink.push_lanes_job(em, leaf, job0 + (uint32_t)r, n);
+        }
+        if (on && !sink.lost) S.maxlen[job0 + (uint32_t)r] = (uint8_t)len;
+        emitted = 15;
+    } else {
+        const int half = l >> 5, b = l & 31;
+        #pragma unroll 1
+        for (int k = 0; k < 15; ++k) {
+            const int r = nd_roll(k);
+            int lo, hi;
+            roll_dice(r, lo, hi);
+            const bool oh = (open >> hi) & 1u, ol = (open >> lo) & 1u;
+            Node th = s0, tl = s0;
+            uint32_t qa = 0u, qb = 0u;
+            if (oh) { th = apply(s0, child(s0, kbar, 31, hi, q), q); qa = gen(th, lo, q, blocked).bits; }
+            if (ol) { tl = apply(s0, child(s0, kbar, 31, lo, q), q); qb = gen(tl, hi, q, blocked).bits; }
+            int len;
+            if (oh && !qa) {                         // pass 1's single entry, the skip rule
+                len = 1;
+                if (!sink.lost) sink.push_lanes_job(1ull, th, job0 + (uint32_t)r, 1);
+                emitted += 1;
+            } else if (!oh && !qb) {                 // pass 2's single entry, or no reply
+                len = ol ? 1 : 0;
+                if (!sink.lost) sink.push_lanes_job(1ull, ol ? tl : s0, job0 + (uint32_t)r, len);
+                emitted += 1;
+            } else {
+                len = 2;
+                if (!oh) qa = 0u;
+                const int eh = entry_point(q, hi), el = entry_point(q, lo);
+                if (((qa >> eh) & 1u) && ((qb >> el) & 1u) && !((s0.blot >> eh) & 1u) && !((s0.blot >> el) & 1u))
+                    qb &= ~(1u << el);                                   // B's chain repeats A's
+                const uint32_t mk = half ? qb : qa;
+                const bool act = b < 24 && ((mk >> b) & 1u);
+                Node leaf = s0;
+                if (act) {
+                    const Node& par = half ? tl : th;
+                    leaf = apply(par, child(par, Kids{mk, -1}, b, half ? hi : lo, q), q);
+                }
+                const uint64_t em = __ballot(act);
+                sink.push_lanes_job(em, leaf, job0 + (uint32_t)r, 2);
+                emitted += (unsigned long long)__popcll(em);
+            }
+            if (l == 0 && !sink.lost) S.maxlen[job0 + (uint32_t)r] = (uint8_t)len;
+        }
+    }
+    SC_CNT(6, 1);
+    if (!sink.lost) leaves += emitted;
+    return 0u;
+}
+
 // All 15 non-doubles rolls of one row in one pass (the 2-ply's set semantics):
 // the first sub-moves of all six dice on the lanes (die d_l, source a_l), each
 // lane's second-level child lists for the five other dice, then the two-steps of
@@ -282,8 +394,9 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
                                            KeySink& sink, unsigned long long& leaves) {
     constexpr uint32_t kAllNd = 0x000B77BEu;        // the 15 non-doubles roll indices
     const int off = (int)((s0.k3 >> 4) & 15u);
-    BG_CNT(1, 1);
-    if ((s0.k3 & 15u) != 0u || 15 - s0.n_home - off < 2) { BG_CNT(3, 1); return kAllNd; }
+    SC_CNT(1, 1);
+    if ((s0.k3 & 15u) != 0u && S.bar_rows) return nd_row_bar(S, row, s0, q, blocked, sink, leaves);
+    if ((s0.k3 & 15u) != 0u || 15 - s0.n_home - off < 2) { SC_CNT(3, 1); return kAllNd; }
     const int l = lane_id();
     uint32_t K[7];
     int st[8];
@@ -294,7 +407,7 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
         st[d + 1] = st[d] + __popc(K[d]);
     }
     const int n1 = st[7];
-    if (n1 > 64) { BG_CNT(3, 1); return kAllNd; }
+    if (n1 > 64) { SC_CNT(3, 1); return kAllNd; }
     // lane l: first sub-move (die dl, source al)
     const bool act = l < n1;
     int dl = 1;
@@ -349,7 +462,7 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
             total += (uint32_t)__popcll(m) << b;
         }
         const int meta = al | (dl << 5) | (r << 8);
-        BG_CNT(5, (total + 63) / 64);
+        SC_CNT(5, (total + 63) / 64);
         for (uint32_t ch = 0; ch < total; ch += 64) {
             const uint32_t pp = ch + (uint32_t)l;
             const bool valid = pp < total;
@@ -382,140 +495,8 @@ __device__ __forceinline__ uint32_t nd_row(const S2& S, int row, const Node& s0,
     }
     // every fast roll has a first pass-1 two-step (emitted): max length 2
     const uint32_t fast = kAllNd & ~slow;
-    BG_CNT(4, __popc(slow));
-    BG_CNT(13, emitted);
-    if (l < 21 && ((fast >> l) & 1u) && !sink.lost) S.maxlen[job0 + (uint32_t)l] = 2;
-    if (!sink.lost) leaves += emitted;
-    return slow;
-}
-
-// nd_row without lane shuffles (round 5).  nd_row's chunk loop moves each chunk lane's
-// parent in with 16 ds_bpermute (a 6-step binary search for the parent, its child list,
-// prefix, node and meta): the counters put the light enumerator at 28 % of its wave time
-// stalled on LDS issue.  Here nothing crosses lanes through LDS:
-// * the parent of chunk position p is found from ballots (chunk_parent, bg_core.h);
-// * the parent's first sub-move (die, source) follows from its lane index and the
-//   wave-uniform per-die child lists, and its node, child list and meta are recomputed
-//   from the uniform root node (no bar, no bear-off in these rows: plain sub-moves).
-// Same leaves, in the same order, as nd_row (tests: BGX_2PLY_NDROW=1 runs nd_row).
-__device__ __forceinline__ void first_move_of(int x, const uint32_t (&K)[7], const int (&st)[8], int& d, int& a,
-                                              uint32_t& kd) {
-    d = 1;
-    #pragma unroll
-    for (int dd = 2; dd <= 6; ++dd) d = x >= st[dd] ? dd : d;
-    kd = K[1];
-    int kst = 0;
-    #pragma unroll
-    for (int dd = 2; dd <= 6; ++dd) { kd = d == dd ? K[dd] : kd; kst = d == dd ? st[dd] : kst; }
-    a = select_bit(kd, x - kst);
-}
-
-__device__ __forceinline__ uint32_t nd_row2(const S2& S, int row, const Node& s0, int q, uint32_t blocked,
-                                            KeySink& sink, unsigned long long& leaves) {
-    constexpr uint32_t kAllNd = 0x000B77BEu;        // the 15 non-doubles roll indices
-    const int off = (int)((s0.k3 >> 4) & 15u);
-    BG_CNT(1, 1);
-    if ((s0.k3 & 15u) != 0u || 15 - s0.n_home - off < 2) { BG_CNT(3, 1); return kAllNd; }
-    const int l = lane_id();
-    uint32_t K[7];
-    int st[8];
-    st[1] = 0;
-    K[0] = 0u;
-    #pragma unroll
-    for (int d = 1; d <= 6; ++d) {
-        K[d] = gen(s0, d, q, blocked).bits;
-        st[d + 1] = st[d] + __popc(K[d]);
-    }
-    const int n1 = st[7];
-    if (n1 > 64) { BG_CNT(3, 1); return kAllNd; }
-    // lane l: first sub-move (die dl, source al)
-    const bool act = l < n1;
-    int dl, al;
-    uint32_t kd;
-    first_move_of(act ? l : 0, K, st, dl, al, kd);
-    Node t1 = s0;
-    uint32_t Q[7];
-    Q[0] = 0u;
-    if (act) t1 = apply(s0, child(s0, Kids{kd, -1}, al, dl, q), q);
-    #pragma unroll
-    for (int e = 1; e <= 6; ++e) Q[e] = act && e != dl ? gen(t1, e, q, blocked).bits : 0u;
-    // roll (hi, lo) is fast iff its pass 1 (hi first) has a two-step
-    uint64_t M[7], N[7];
-    #pragma unroll
-    for (int d = 1; d <= 6; ++d) { M[d] = __ballot(act && dl == d); N[d] = __ballot(Q[d] != 0u); }
-    uint32_t slow = 0u;
-    #pragma unroll
-    for (int hi = 2; hi <= 6; ++hi)
-        #pragma unroll
-        for (int lo = 1; lo < hi; ++lo)
-            if (!(M[hi] & N[lo])) slow |= 1u << (roll_start(lo) + hi - lo);
-    const int sg = q == 0 ? 1 : -1;
-    const uint32_t root_occ = s0.occ, root_blot = s0.blot;
-    const uint32_t job0 = (uint32_t)row * 21u;
-    unsigned long long emitted = 0;
-    // a parent's two-steps with second die e (its child list for e, masked as nd_row)
-    auto kids_e = [&](const Node& t, int d, int a, int e) -> uint32_t {
-        const int hi = d > e ? d : e, lo = d > e ? e : d;
-        const int r = roll_start(lo) + hi - lo;
-        if (d == e || ((slow >> r) & 1u)) return 0u;
-        uint32_t c = gen(t, e, q, blocked).bits;
-        if (d < e) c &= 1u << (a + sg * d);
-        return c;
-    };
-    #pragma unroll 1
-    for (int e = 1; e <= 6; ++e) {
-        // the lane's first-level node again (cheaper than holding it across the loop)
-        const Node t1e = apply(s0, child(s0, Kids{kd, -1}, al, dl, q), q);
-        const uint32_t c = act ? kids_e(t1e, dl, al, e) : 0u;
-        const uint32_t cnt = (uint32_t)__popc(c);
-        uint32_t pre = 0, total = 0;
-        const uint64_t below = (1ull << l) - 1ull;
-        #pragma unroll
-        for (int b = 0; b < 5; ++b) {
-            const uint64_t m = __ballot((cnt >> b) & 1u);
-            pre += (uint32_t)__popcll(m & below) << b;
-            total += (uint32_t)__popcll(m) << b;
-        }
-        BG_CNT(5, (total + 63) / 64);
-        int carry_src = 0;
-        uint32_t carry_pre = 0;
-        for (uint32_t ch = 0; ch < total; ch += 64) {
-            uint32_t psrc;
-            const int src = chunk_parent(cnt, pre, ch, carry_src, carry_pre, &psrc);
-            const uint32_t pp = ch + (uint32_t)l;
-            const bool valid = pp < total;
-            Node leaf = s0;
-            bool emit = false;
-            int pr = 0;
-            if (valid) {
-                int pd, pa;
-                uint32_t pk;
-                first_move_of(src, K, st, pd, pa, pk);
-                const Node s1 = apply(s0, child(s0, Kids{pk, -1}, pa, pd, q), q);
-                const uint32_t qb = kids_e(s1, pd, pa, e);
-                const int hi = pd > e ? pd : e, lo = pd > e ? e : pd;
-                pr = roll_start(lo) + hi - lo;
-                const int cb = select_bit(qb, (int)(pp - psrc));
-                const Sub m = child(s1, Kids{qb, -1}, cb, e, q);
-                leaf = apply(s1, m, q);
-                if (pd > e) {               // pass 1: (pa, hi = pd) then (cb, lo = e)
-                    const int dst_a = pa + sg * pd;
-                    const bool chain = cb == dst_a, rev = m.dst == pa;
-                    emit = (!chain && !rev) ||
-                           nd_first_of(chain ? pa : cb, chain ? 1 : 2, e, pd, q, root_occ, root_blot, blocked);
-                } else {                    // pass 2: (pa, lo = pd) then its chain (cb, hi = e)
-                    emit = nd_first_of(pa, 3, pd, e, q, root_occ, root_blot, blocked);
-                }
-            }
-            const uint64_t em = __ballot(valid && emit);
-            sink.push_lanes_job(em, leaf, job0 + (uint32_t)pr, 2);
-            emitted += (unsigned long long)__popcll(em);
-        }
-    }
-    // every fast roll has a first pass-1 two-step (emitted): max length 2
-    const uint32_t fast = kAllNd & ~slow;
-    BG_CNT(4, __popc(slow));
-    BG_CNT(13, emitted);
+    SC_CNT(4, __popc(slow));
+    SC_CNT(13, emitted);
     if (l < 21 && ((fast >> l) & 1u) && !sink.lost) S.maxlen[job0 + (uint32_t)l] = 2;
     if (!sink.lost) leaves += emitted;
     return slow;
@@ -555,8 +536,7 @@ __device__ __forceinline__ KeySink make_sink(const S2& S) {
 }
 
 // VARIANT 0: jobs (row, non-doubles roll) implicit, 1: (row, doubles roll)
-// implicit, 2: the explicit list, 3: as 0 with the row-level walk (nd_row) first,
-// 4: as 3 with nd_row2.
+// implicit, 2: the explicit list, 3: as 0 with the row-level walk (nd_row) first.
 template <int LOG, int MK, int VARIANT, int WPE = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_enum(S2 S) {
     __shared__ uint4 tab[1 << LOG];
@@ -564,7 +544,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     uint4* memo = MK >= 0 ? memo_ : nullptr;
     KeySink sink = make_sink(S);
     unsigned long long leaves = 0;
-    const int cap = VARIANT == 0 || VARIANT >= 3 ? S.cap_light : S.cap_heavy;
+    const int cap = VARIANT == 0 || VARIANT == 3 ? S.cap_light : S.cap_heavy;
     auto done = [&](int st, int job) {
         if (st == 1) {
             const int qo = LOG < 10 ? 0 : 1;
@@ -590,26 +570,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             int q;
             uint32_t blocked;
             const Node sq = row_node(bv, q, blocked);
-            if (VARIANT >= 3) {
+            if (VARIANT == 3) {
                 // the row-level walk; what it leaves (and a lost pool block: the
                 // whole row again) runs per job
-                BG_T0(t0);
-                uint32_t left = VARIANT == 4 ? nd_row2(S, row, sq, q, blocked, sink, leaves)
-                                             : nd_row(S, row, sq, q, blocked, sink, leaves);
-                BG_T1(9, t0);
+                SC_T0(t0);
+                uint32_t left = nd_row(S, row, sq, q, blocked, sink, leaves);
+                SC_T1(9, t0);
                 if (sink.lost) left = 0x000B77BEu;
-                BG_T0(t1);
+                SC_T0(t1);
                 #pragma unroll 1
                 for (; left; left &= left - 1u) {
                     const int r = __builtin_ctz(left);
                     const int job = row * 21 + r;
-                    BG_CNT(11, 1);
+                    SC_CNT(11, 1);
                     done(enum_job<LOG, uint4*, MK, 0>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves), job);
                 }
-                BG_T1(10, t1);
+                SC_T1(10, t1);
             } else {
                 constexpr int nr = VARIANT == 0 ? 15 : 6;
-                BG_T0(t2);
+                SC_T0(t2);
                 #pragma unroll 1
                 for (int k = 0; k < nr; ++k) {
                     const int r = VARIANT == 0 ? nd_roll(k) : roll_start(k + 1);
@@ -617,7 +596,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                     done(enum_job<LOG, uint4*, MK, VARIANT>(S, job, r, q, sq, blocked, tab, cap, memo, sink, leaves),
                          job);
                 }
-                BG_T1(12, t2);
+                SC_T1(12, t2);
             }
             bv = bv_next;
         }
@@ -1029,7 +1008,11 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
     // narrow: the row parts are loaded first and added after the MFMAs (their latency hidden
     // behind them; 15.9 vs 31.5 ms per C4 batch at H = 40); wide: they start the accumulators
     // (30.6 vs 31.4 ms at H = 128)
+#ifdef BGX_PAIR_LATE
+    constexpr bool kLate = true;
+#else
     constexpr bool kLate = !kWide;
+#endif
     float4 rpv[NN][NA][kWide ? 4 : 2];
     if constexpr (kLate) {
     #pragma unroll
@@ -1066,10 +1049,18 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
             if constexpr (kWide) {
                 const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * NA + t) * 2 + 0) * 64 + l + z]);
                 const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * NA + t) * 2 + 1) * 64 + l + z]);
+#ifdef BGX_PAIR_NOP
+                __builtin_amdgcn_sched_barrier(0);
+                __asm__ volatile("s_nop 4" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+#endif
                 #pragma unroll
                 for (int n = 0; n < NN; ++n) {
                     x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f[n], first ? (f32x16){} : x[n][t], 0, 0, 0);
                     x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f[n], x[n][t], 0, 0, 0);
+#ifdef BGX_PAIR_SPLIT
+                    __builtin_amdgcn_sched_barrier(0);
+#endif
                 }
             } else {
                 const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + t) * 64 + l + z]);
@@ -1754,9 +1745,11 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
                            lane_off, &ctr->rows, rowrec, rowside, nullptr, &ctr->bad);
         SCK(hipGetLastError());
+        const char* brw = getenv("BGX_2PLY_BARROW");      // tests: the bar rows per job instead
         S2 S{rowrec, 0, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
-             retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>(), 3, 3};
+             retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>(), 3, 3,
+             brw && brw[0] == '0' ? 0 : 1};
         // doubles enumerator: 512-slot dedup table with the revisit memo inside it, held to
         // 128 VGPRs (4 waves/SIMD, +1.5 %).  Tests (BGX_2PLY_HEAVY = 9:0 / 10:0) run the
         // exact alternatives without the memo (9:0) or with a 1,024-slot table (10:0): the
@@ -1788,13 +1781,9 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
                                0, s, rowside, &ctr->rows, w1q, rowpart);
         EvalArgs E{nullptr, nullptr, &ctr->zero, &ctr->cursor, 0ull, rowside, maxlen, minv,
                    w1q, f16s + 4 + kKB * slices(NT) * 64 * 4, value_bias, factored ? rowpart : nullptr, nullptr};
-        // the non-doubles enumerator: the shuffle-free row walk (nd_row2) held to 96 VGPRs
-        // (5 waves/SIMD; at 80 it spills).  BGX_2PLY_NDROW=1 (tests, A/B): the round-4 row
-        // walk with lane shuffles (nd_row, 80 VGPRs: 6 waves/SIMD); =6: nd_row2 at 80 VGPRs
-        const char* ndr = getenv("BGX_2PLY_NDROW");
-        void (*klight)(S2) = k_enum<kLogLight, -1, 4, 5>;
-        if (ndr && ndr[0] == '1') klight = k_enum<kLogLight, -1, 3, 6>;
-        else if (ndr && ndr[0] == '6') klight = k_enum<kLogLight, -1, 4, 6>;
+        // the non-doubles enumerator: the row-level walk held to 80 VGPRs (6 waves/SIMD,
+        // +1.2 % over its natural 91)
+        void (*klight)(S2) = k_enum<kLogLight, -1, 3, 6>;
         const int g_light = persistent_grid(e, klight, 32);
         const int g_heavy = persistent_grid(e, kheavy, 32);
         const int g_list = persistent_grid(e, klist, 32);
@@ -1941,9 +1930,9 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
 // this translation unit's work counters (experiments; bg_engine.hip has its own set)
 int bgx_debug_search_counters(unsigned long long* out16) {
     SCK(hipDeviceSynchronize());
-    SCK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bg::g_cnt), 16 * 8));
+    SCK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_scnt), 16 * 8));
     unsigned long long z[16] = {0};
-    SCK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z, 16 * 8));
+    SCK(hipMemcpyToSymbol(HIP_SYMBOL(g_scnt), z, 16 * 8));
     return BGX_OK;
 }
 #endif

@@ -229,9 +229,10 @@ def test_two_ply_full_batch_paths_agree(monkeypatch):
     """C4 at full size (B = 65,536 roots after 60 self-play steps): the doubles
     enumerator with its revisit memo inside a 512-slot table and with a
     1,024-slot table plus separate memo tables (different tier traffic, pruning
-    and pool block order), and the non-doubles row walk with and without lane
-    shuffles, give bit-identical Q, the same choices and the same surviving-leaf
-    counts; every choice is a legal move and every Q is finite."""
+    and pool block order), and the replies of rows whose replier is on the bar as one
+    table-free row walk or as 15 per-job walks, give bit-identical Q, the same choices
+    and the same surviving-leaf counts; every choice is a legal move and every Q is
+    finite."""
     import bgx
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead, two_ply
@@ -249,10 +250,10 @@ def test_two_ply_full_batch_paths_agree(monkeypatch):
     assert s1 == s2
     assert torch.equal(torch.nan_to_num(Q1, 7.0), torch.nan_to_num(Q2, 7.0))
     assert torch.equal(b1, b2) and torch.equal(q1, q2)
-    # the round-4 non-doubles row walk with lane shuffles (nd_row) against the default
-    # shuffle-free one (nd_row2): the same leaves
+    # the rows whose replier is on the bar: the table-free row walk (nd_row_bar) against
+    # the per-job walks it replaces
     monkeypatch.delenv("BGX_2PLY_HEAVY")
-    monkeypatch.setenv("BGX_2PLY_NDROW", "1")
+    monkeypatch.setenv("BGX_2PLY_BARROW", "0")
     b3, q3, Q3, s3 = two_ply(eng, vh, want_q=True)
     assert s1 == s3
     assert torch.equal(torch.nan_to_num(Q1, 7.0), torch.nan_to_num(Q3, 7.0))

@@ -4,9 +4,10 @@
     python tools/enum_counters.py [--age 180]      # on the GPU: one C4 batch, counters printed
 
 Counters (csrc/bg_search.hip BG_CNT / BG_T1, s_memtime ticks are 100 MHz):
-  1 rows entering nd_row, 3 rows sent to per-job walks at entry (bar / bear-off / > 64
-  first moves), 4 slow rolls of fast rows, 5 nd_row chunks, 13 two-steps emitted by
-  nd_row, 9 ticks in nd_row, 10 ticks in the light enumerator's per-job walks, 11 those
+  1 rows entering nd_row, 3 rows sent to per-job walks at entry (bear-off possible / > 64
+  first moves), 6 rows of nd_row_bar (replier on the bar), 8 their slow rolls, 4 slow
+  rolls of nd_row's fast rows, 5 nd_row chunks, 13 two-steps emitted by nd_row, 9 ticks
+  in nd_row (+ nd_row_bar), 10 ticks in the light enumerator's per-job walks, 11 those
   jobs, 12 ticks in the doubles enumerator's per-row job loops.
 """
 import argparse
@@ -21,6 +22,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "mlp-ppo-2ply-p3_amd")
 LIB = os.path.join(PKG, "bgx", "libbgx_cnt.so")
 NAMES = {1: "nd_rows", 3: "nd_rows_rejected", 4: "slow_rolls_in_fast_rows", 5: "nd_chunks",
+         6: "bar_rows", 8: "slow_rolls_in_bar_rows",
          13: "nd_two_steps_emitted", 9: "ticks_nd_row", 10: "ticks_light_per_job", 11: "light_per_job_jobs",
          12: "ticks_doubles_rows"}
 
