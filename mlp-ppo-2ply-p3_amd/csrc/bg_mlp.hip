@@ -181,7 +181,25 @@ __host__ __device__ inline void views(P base, int T, int OT, P& hdr, P& w1q, P& 
 // waves, unskipped.  Outputs equal the unskipped kernel's up to the log-sum-exp's
 // summation order (the noise is keyed by (row, action)); BGX_POLICY_SKIP=0 turns
 // the skip off.  MODE 0 workgroups are 4 waves: 4 x 32 rows, or one gathered set.
+// Round 5: the extra workgroups also take the rows with more than skip_arg (64) legal
+// actions (BGX_POLICY_HEAVY), so no main wave walks more than 2 action tiles plus the
+// value tile: per-wave stamps (tools/policy_stamps.py) showed the main waves of a
+// 16,384-row launch at 12.6 us of output tiles on average but 36 us for the slowest --
+// a 32-row group holding a doubles row with hundreds of legal moves walks all 16 tiles
+// alone -- and that wave set the launch at 45.7 us; now 20.3 us (C3 380 -> 412 M env
+// steps/s; 32 is worse: the 64-row windows of the extra workgroups overflow).
 constexpr int kZWin = 256, kZCap = 64;
+constexpr int kHeavyDefault = 64;
+
+#ifdef BGX_POLICY_STAMPS
+// experiment: per-wave s_memrealtime stamps of the rollout policy kernel (tools/policy_stamps.py)
+// [wave][6]: start, after the count-0 scan + staging, after GEMM1, end, flags (extra | main), tiles
+constexpr int kStampWaves = 8192;
+__device__ unsigned long long g_pstamp[kStampWaves][6];
+#define PSTAMP(k) do { if (MODE == 0 && sw < kStampWaves && lane_id() == 0) g_pstamp[sw][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PSTAMP(k) do { } while (0)
+#endif
 constexpr float kSkipMargin = 30.0f;
 
 template <int T, int MODE>
@@ -192,6 +210,10 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
                                                    int32_t* act_out, float* logp_out, float* value_out,
                                                    float* logits_arg, uint8_t* records_out, int skip_arg) {
     // the noise's step: the argument, plus a device counter when given (a replayed graph)
+#ifdef BGX_POLICY_STAMPS
+    const int sw = (int)(blockIdx.x * (MODE == 0 ? 4 : 1) + (threadIdx.x >> 6));
+#endif
+    PSTAMP(0);
     const uint32_t step = step_arg + (step_ctr ? *step_ctr : 0u);
     constexpr int kW = MODE == 0 ? 4 : 1;              // waves per workgroup
     const bool greedy = MODE < 0 ? greedy_arg != 0 : false;
@@ -224,7 +246,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
         #pragma unroll
         for (int k = 0; k < kZWin / 64; ++k) {
             const int r = base + 64 * k + l;
-            const bool z = r < n && cw[k] == 0;
+            const bool z = r < n && (cw[k] == 0 || (int)cw[k] > skip_arg);
             const uint64_t m = __ballot(z);
             const int pos = nzw + __popcll(m & ((1ull << l) - 1ull));
             if (extra && wv == 0 && z && pos < kZCap) zl[pos] = r;
@@ -234,7 +256,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
     const int kx = extra ? ((int)blockIdx.x & 1) : 0;
     const int nz = extra ? min(nzw - 32 * kx, 32) : 32;       // rows of this wave (extra: gathered)
     if (extra && (nzw > kZCap || nz <= 0)) return;             // uniform in the workgroup
-    const bool self_zero = skip_on && !extra && nzw > kZCap;   // count-0 rows stay on the main wave
+    const bool self_zero = skip_on && !extra && nzw > kZCap;   // gathered rows stay on the main wave
     const int vt = n_actions >> 5;                     // the tile holding the value output
     if (extra) __syncthreads();                        // zl
     // stage 32 records (2 KiB, this wave's own copy): lane l copies 32 bytes
@@ -255,12 +277,15 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
     if (kW > 1) __builtin_amdgcn_wave_barrier(); else __syncthreads();
     const uint8_t* myrec = srec + j * 64;
     const int count = (int)myrec[60] | ((int)myrec[61] << 8);
+    // this row is an extra workgroup's (count 0, or more than skip_arg legal actions)
+    const bool gathered = skip_on && !extra && !self_zero && (count == 0 || count > skip_arg);
     const bool row_ok = extra ? j < nz : row0 + j < n;
     const int grow = extra ? zl[32 * kx + (j < nz ? j : 0)] : row0 + j;
     // output tiles of this wave: all (main), a quarter (extra)
     const int per = extra ? (n_otiles + kW - 1) / kW : n_otiles;
     const int o_beg = extra ? min(wv * per, n_otiles) : 0, o_end = extra ? min(o_beg + per, n_otiles) : n_otiles;
 
+    PSTAMP(1);
     // ---- GEMM1: X1s[t] = W1s[32t.., :] . F^T + b1 * 2^e1  (= 2^e1 X1)
     f32x16 x1[T];
     #pragma unroll
@@ -307,7 +332,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
     int o_s = n_otiles;
     float ub = INFINITY;
     if (skip_on && !extra) {
-        int cm = count;
+        int cm = gathered ? 0 : count;
         #pragma unroll
         for (int d = 1; d < 32; d <<= 1) cm = max(cm, __shfl_xor(cm, d));
         o_s = max((cm + 31) >> 5, 1);
@@ -331,6 +356,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
     const int E = e2 + e1 + ex;
     const float up = ldexpf(1.0f, E), down = ldexpf(1.0f, -E);
 
+    PSTAMP(2);
     // ---- GEMM2 per 32-output tile + online masked log-sum-exp + Gumbel-max
     // (branch-free: outputs that are not actions of this lane enter as -inf)
     float m = -INFINITY, s = 0.0f, best = -INFINITY, bestz = 0.0f, value = 0.0f;
@@ -403,7 +429,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
         int next = o + 1;
         if (at_s) {
             const float m_row = fmaxf(m, __shfl_xor(m, 32)), b_row = fmaxf(best, __shfl_xor(best, 32));
-            const bool ok = (count == 0 && !self_zero) || (ub + kMaskLog < m_row - kSkipMargin && ub + kMaskLog + kGumbelMax < b_row);
+            const bool ok = gathered || (ub + kMaskLog < m_row - kSkipMargin && ub + kMaskLog + kGumbelMax < b_row);
             if (__ballot(!ok) == 0ull) {
                 next = vt;
             } else {                                   // no skip: tile o + 1 after all
@@ -437,6 +463,10 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
             value += pm[q][4][l];
         }
     }
+    PSTAMP(3);
+#ifdef BGX_POLICY_STAMPS
+    if (MODE == 0 && sw < kStampWaves && lane_id() == 0) g_pstamp[sw][4] = extra ? 1 : 2;
+#endif
     // combine the two lane halves of each row (lanes j and j+32)
     const float m2 = __shfl_xor(m, 32), s2 = __shfl_xor(s, 32);
     const float best2 = __shfl_xor(best, 32), bestz2 = __shfl_xor(bestz, 32);
@@ -449,7 +479,7 @@ __global__ __launch_bounds__(MODE == 0 ? 256 : 64) __attribute__((amdgpu_waves_p
     const float z_fin = take2 ? bestz2 : bestz;
     const float v_fin = h == 0 ? value + value2 : 0.0f;   // the value row sits in exactly one half
     // count-0 rows of the main waves belong to the extra waves
-    if (h == 0 && row_ok && (extra || !skip_on || self_zero || count != 0)) {
+    if (h == 0 && row_ok && !gathered) {
         act_out[grow] = a_fin;
         // Categorical.log_prob = log(clamp(p, eps, 1 - eps)) (torch clamp_probs), in the log domain
         if (logp_out) logp_out[grow] = fminf(fmaxf(z_fin - (mm + logf(ss)), -15.942384719848633f),
@@ -693,6 +723,16 @@ int bgx_policy_pack(const float* W1, const float* b1, const float* Wa, const flo
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }
 
+#ifdef BGX_POLICY_STAMPS
+extern "C" int bgx_debug_policy_stamps(unsigned long long* out, int32_t waves) {
+    if (hipDeviceSynchronize() != hipSuccess) return BGX_EDEVICE;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamp), (size_t)(waves < kStampWaves ? waves : kStampWaves) * 48) != hipSuccess)
+        return BGX_EDEVICE;
+    static unsigned long long z[kStampWaves][6];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pstamp), z, sizeof z) == hipSuccess ? BGX_OK : BGX_EDEVICE;
+}
+#endif
+
 int bgx_policy_act_ctr(const uint8_t* records_dev, int32_t n, const float* packed, int32_t hidden, int32_t n_actions,
                        uint64_t seed, uint32_t step, const uint32_t* step_ctr, int32_t greedy, int32_t* act_out,
                        float* logp_out, float* value_out, float* logits_out, uint8_t* records_out, void* stream) {
@@ -709,13 +749,17 @@ int bgx_policy_act_ctr(const uint8_t* records_dev, int32_t n, const float* packe
     // the masked-action tile skip (k_policy_act, MODE 0): 2 extra waves per kZWin rows for count-0 rows
     const char* sv = getenv("BGX_POLICY_SKIP");     // read per call: tests compare both paths in one process
     const bool skip = !(sv && sv[0] == '0');
+    // rows with more legal actions than this go to the extra workgroups too (their tiles split
+    // four ways), so no main wave walks more than ceil(heavy / 32) action tiles (round 5)
+    const char* hv = getenv("BGX_POLICY_HEAVY");
+    const int heavy = hv ? atoi(hv) : kHeavyDefault;
     const dim3 grid0(skip ? n_wg + 2 * ((n + kZWin - 1) / kZWin) : n_wg);
 #define BGX_ACT(TT)                                                                                           \
     do {                                                                                                      \
         if (plain)                                                                                            \
             hipLaunchKernelGGL((k_policy_act<TT, 0>), grid0, dim3(256), 0, s, records_dev, n, packed, n_actions, OT, \
                                lo, hi, step, step_ctr, greedy, act_out, logp_out, value_out, logits_out,     \
-                               records_out, skip ? 1 : 0);                                                    \
+                               records_out, skip ? (heavy > 0 ? heavy : 1) : 0);                             \
         else                                                                                                  \
             hipLaunchKernelGGL((k_policy_act<TT, -1>), grid, blk, 0, s, records_dev, n, packed, n_actions, OT,   \
                                lo, hi, step, step_ctr, greedy, act_out, logp_out, value_out, logits_out,     \

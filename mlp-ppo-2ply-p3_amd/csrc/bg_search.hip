@@ -275,7 +275,13 @@ __device__ __forceinline__ int enum_job(const S2& S, int job, int r, int q, cons
     g.sink.job = (uint32_t)job;
     g.sink.lost = false;
     if (KIND == 0) g.run_nd(sq, r0, r1);
-    else if (KIND == 1) g.run_d(sq, r0);
+    else if (KIND == 1) {
+        SC_T0(tdd);
+        g.run_d(sq, r0);
+        if ((sq.k3 & 15u) != 0u) { SC_CNT(7, 1); SC_T1(15, tdd); }
+        else if (g.pure_walk) { SC_CNT(2, 1); SC_T1(14, tdd); }
+        else SC_T1(0, tdd);
+    }
     else g.run(sq, r0, r1);
     if (!g.ovf && g.count == 0) g.sink.push(sq, 0ull, 0, 0);     // no reply: the leaf is a itself
     sink = g.sink;
@@ -1928,11 +1934,13 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
 
 #ifdef BGX_COUNTERS
 // this translation unit's work counters (experiments; bg_engine.hip has its own set)
-int bgx_debug_search_counters(unsigned long long* out16) {
+int bgx_debug_search_counters(unsigned long long* out32) {
     SCK(hipDeviceSynchronize());
-    SCK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_scnt), 16 * 8));
+    SCK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_scnt), 16 * 8));
+    SCK(hipMemcpyFromSymbol(out32 + 16, HIP_SYMBOL(bg::g_cnt), 16 * 8));   // the move generator's (bg_core.h)
     unsigned long long z[16] = {0};
     SCK(hipMemcpyToSymbol(HIP_SYMBOL(g_scnt), z, 16 * 8));
+    SCK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z, 16 * 8));
     return BGX_OK;
 }
 #endif

@@ -197,12 +197,16 @@ def _assert_same(on, off, rec):
         assert d[zero].max().item() < 4 * TOL
 
 
-def test_policy_tile_skip_matches_full_pass(bgx, monkeypatch):
-    """The masked-action tile skip and the count-0 extra waves (bg_mlp.hip,
-    k_policy_act MODE 0) give the outputs of the full 16-tile pass: self-play
-    positions (count-0 rows, doubles with hundreds of moves), a window with more
-    count-0 rows than the extra waves take, a ragged batch, and weights whose
-    logit bound is too loose for any skip."""
+@pytest.mark.parametrize("heavy", ["64", "32", "1000"])
+def test_policy_tile_skip_matches_full_pass(bgx, monkeypatch, heavy):
+    """The masked-action tile skip and the extra waves (bg_mlp.hip, k_policy_act MODE 0:
+    rows with no legal move or more than BGX_POLICY_HEAVY legal actions gathered into
+    workgroups that split the action tiles four ways; 1000 = count-0 rows only, the
+    round-4 form) give the outputs of the full 16-tile pass: self-play positions
+    (count-0 rows, doubles with hundreds of moves), a window with more gathered rows
+    than the extra waves take, a ragged batch, and weights whose logit bound is too
+    loose for any skip."""
+    monkeypatch.setenv("BGX_POLICY_HEAVY", heavy)
     from bgx.policy import PolicyNet
     torch.manual_seed(0)
     net = PolicyNet(hidden_size=128).cuda()

@@ -24,7 +24,13 @@ LIB = os.path.join(PKG, "bgx", "libbgx_cnt.so")
 NAMES = {1: "nd_rows", 3: "nd_rows_rejected", 4: "slow_rolls_in_fast_rows", 5: "nd_chunks",
          6: "bar_rows", 8: "slow_rolls_in_bar_rows",
          13: "nd_two_steps_emitted", 9: "ticks_nd_row", 10: "ticks_light_per_job", 11: "light_per_job_jobs",
-         12: "ticks_doubles_rows"}
+         12: "ticks_doubles_rows", 0: "ticks_doubles_table_walks", 2: "doubles_pure_walks", 14: "ticks_doubles_pure",
+         7: "doubles_bar_jobs", 15: "ticks_doubles_bar",
+         # bg_core.h's move-generator counters (+16)
+         16: "core_doubles_calls", 17: "core_ticks_doubles", 18: "core_place_batches", 19: "core_depth2_fresh",
+         21: "core_depth3_fresh", 22: "core_flat_leaves_calls", 23: "core_flat_leaves_children", 24: "core_commit_n",
+         25: "core_ticks_doubles_to_got4", 26: "core_got4", 27: "core_ticks_push", 28: "core_ticks_probe",
+         29: "core_ticks_place", 30: "core_depth2_children", 31: "core_depth3_children"}
 
 
 def build():
@@ -77,12 +83,12 @@ def main():
     torch.manual_seed(1)
     vh = ValueHead(PolicyNet(hidden_size=a.hidden).to(dev))
     two_ply(eng, vh)
-    c = (ctypes.c_ulonglong * 16)()
+    c = (ctypes.c_ulonglong * 32)()
     fn(ctypes.cast(c, ctypes.c_void_p))              # reset
     _, _, _, st = two_ply(eng, vh)
     te, tv = two_ply_timings(eng)
     fn(ctypes.cast(c, ctypes.c_void_p))
-    out = {NAMES.get(i, f"c{i}"): int(c[i]) for i in range(16) if c[i]}
+    out = {NAMES.get(i, f"c{i}"): int(c[i]) for i in range(32) if c[i]}
     out.update({"stats": st, "enumeration_ms": te, "evaluation_ms": tv, "age": a.age, "hidden": a.hidden})
     print(json.dumps(out))
 
