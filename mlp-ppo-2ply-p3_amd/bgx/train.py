@@ -345,10 +345,11 @@ PPO_GW2_TASK_TILES = 32        # include/bgx.h BGX_PPO_GW2_TASK_TILES
 FEAT_BIAS_COL = 198            # the ones column of the 208-wide rows: gW1[:, 198] = gb1
 
 
-def ppo_row_plan(records: torch.Tensor, n_actions: int = 500):
+def ppo_row_plan(records: torch.Tensor, n_actions: int = 500, out=None):
     """ppo_row_plan_torch on the GPU as three HIP launches (bgx_ppo_plan: a stable
     counting sort by class plus the plan from the class totals), no host sync; the
-    torch form on the CPU."""
+    torch form on the CPU.  out: (perm int32[m], plan int32[33], row_plan int32[8])
+    to write into (the graphed update's persistent buffers)."""
     if not records.is_cuda:
         return ppo_row_plan_torch(records, n_actions)
     m = records.shape[0]
@@ -356,9 +357,12 @@ def ppo_row_plan(records: torch.Tensor, n_actions: int = 500):
     dev = records.device
     rec = records.contiguous()
     ws = torch.empty(max(int(L.bgx_ppo_plan_workspace(m)) // 4, 1), dtype=torch.int32, device=dev)
-    perm = torch.empty(m, dtype=torch.int32, device=dev)
-    plan = torch.empty(33, dtype=torch.int32, device=dev)
-    row_plan = torch.empty(8, dtype=torch.int32, device=dev)
+    if out is not None:
+        perm, plan, row_plan = out
+    else:
+        perm = torch.empty(m, dtype=torch.int32, device=dev)
+        plan = torch.empty(33, dtype=torch.int32, device=dev)
+        row_plan = torch.empty(8, dtype=torch.int32, device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     check(L.bgx_ppo_plan(p(rec), m, n_actions, p(ws), p(perm), p(plan), p(row_plan),
                          ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "bgx_ppo_plan")
@@ -394,10 +398,11 @@ def ppo_row_plan_torch(records: torch.Tensor, n_actions: int = 500):
     return perm, torch.cat([pre, start]).to(torch.int32).contiguous(), row_plan
 
 
-def gather_rollout(perm, recs, acts, old, R, adv):
+def gather_rollout(perm, recs, acts, old, R, adv, out=None):
     """Rows perm[i] of the records and the four per-row fields, in one HIP kernel on the
     GPU (bgx_gather_rollout; torch's index gathers of the [m, 64] records ran at ~1 TB/s),
-    the torch gathers elsewhere.  Returns (records, actions, old_logp, returns, adv)."""
+    the torch gathers elsewhere.  Returns (records, actions, old_logp, returns, adv),
+    written into `out` when given."""
     acts, old, R, adv = (acts.to(torch.int32).contiguous(), old.float().contiguous(), R.float().contiguous(),
                          adv.float().contiguous())
     recs = recs.contiguous()
@@ -405,8 +410,9 @@ def gather_rollout(perm, recs, acts, old, R, adv):
         pl = perm.long()
         return recs[pl].contiguous(), acts[pl], old[pl], R[pl], adv[pl]
     m = perm.shape[0]
-    out = (torch.empty_like(recs), torch.empty_like(acts), torch.empty_like(old), torch.empty_like(R),
-           torch.empty_like(adv))
+    if out is None:
+        out = (torch.empty_like(recs), torch.empty_like(acts), torch.empty_like(old), torch.empty_like(R),
+               torch.empty_like(adv))
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     check(_lib.load().bgx_gather_rollout(p(perm.to(torch.int32).contiguous()), m, p(recs), p(acts), p(old), p(R), p(adv),
                                          *[p(t) for t in out],
@@ -609,7 +615,7 @@ class PPOTrainer:
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
                  chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True,
                  entropy_anneal: str = "train", shards: int | None = None, graphs: bool | None = None,
-                 fork: bool | None = None, streams=None):
+                 fork: bool | None = None, streams=None, update_graphs: bool | None = None):
         if entropy_anneal not in ("train", "train_single"):
             raise ValueError(f"entropy_anneal must be 'train' or 'train_single', got {entropy_anneal!r}")
         self.entropy_anneal = entropy_anneal
@@ -646,6 +652,19 @@ class PPOTrainer:
         # shard's copy stream, beside the next pair's steps.
         self.graphs = (self.dev.type == "cuda" and horizon % 2 == 0) if graphs is None else graphs
         self._graphs = None
+        # the update's fused-head epoch replayed as a HIP graph (round 5): one eager epoch
+        # issues ~50 small torch launches between the big kernels, and the GPU idled 1.4 ms
+        # per update waiting for the host (profiles/r5/update_trace_plan.txt).  The graph is
+        # captured at the second update (the first initialises the Adam and GradScaler
+        # state eagerly) over persistent row buffers, and again when its host-side inputs
+        # change: the GradScaler scale (a growth or a skipped step) or the entropy
+        # coefficient.  Not with a process group (collectives stay eager).
+        self.update_graphs = ((self.dev.type == "cuda" and _world(process_group) == 1
+                               and not (dist.is_available() and dist.is_initialized()))
+                              if update_graphs is None else bool(update_graphs))
+        self._ugraph = None            # (key, graph, loss-parts output)
+        self._ubufs = None             # persistent per-chunk rows in plan order + plans
+        self._updates_done = 0
         # fork (Engine.set_fork): an env step's light launch on the engine's side stream.
         # Off by default with graphs: each shard's graph is then one linear chain on its own
         # hardware queue (forked graphs' internal streams share queues with the other
@@ -835,7 +854,10 @@ class PPOTrainer:
             parts = self._epochs(recs, acts, old, R, adv, False)
         else:
             snap = self._snapshot()
-            guard = torch.zeros((), dtype=torch.bool, device=self.dev)
+            if getattr(self, "_guard", None) is None:       # persistent: a captured epoch writes it
+                self._guard = torch.zeros((), dtype=torch.bool, device=self.dev)
+            guard = self._guard
+            guard.zero_()
             hint = self._scale_state()
             parts = self._epochs(recs, acts, old, R, adv, True, guard, scale_hint=hint)
             if hint is not None and self._scale_state() != hint:
@@ -855,6 +877,7 @@ class PPOTrainer:
                 self.fused_head = False
                 parts = self._epochs(recs, acts, old, R, adv, False)
         self.entropy_coef = entropy_coef_after_update(self.entropy_anneal, self.total_episodes)
+        self._updates_done += 1
         p = (parts / NUM_EPOCHS).tolist()
         return {"policy_loss": p[0], "value_loss": p[1], "entropy": p[2], "total_loss": p[3]}
 
@@ -879,6 +902,10 @@ class PPOTrainer:
                  for s in range(0, N, self.chunk)] if self.fused else None
         preps = [{} for _ in range(0, N, self.chunk)]
         sorted_rows = [None for _ in range(0, N, self.chunk)]
+        graphed = (fused_head and manual and self.update_graphs and guard is not None and scale_hint is not None
+                   and self._updates_done >= 1)
+        if graphed:
+            return self._epochs_graphed(recs, acts, old, R, adv, guard, scale_hint)
         if fused_head:
             # once per update: each chunk's rows in the order of the fused head's row plan
             # (by the number of action tiles a row needs), gathered so that every kernel
@@ -908,6 +935,63 @@ class PPOTrainer:
                           amp=self.amp, fused=self.fused, sync=False, guard=guard, fused_head=fused_head,
                           scale_hint=scale_hint)
             parts = e if parts is None else parts + e
+        return parts
+
+    def _epochs_graphed(self, recs, acts, old, R, adv, guard, hint):
+        """_epochs' fused-head epochs as HIP-graph replays: the rows go into persistent
+        plan-order buffers (eager), one epoch is captured per (GradScaler scale, entropy
+        coefficient) and replayed NUM_EPOCHS times; the host's copy of the scaler state
+        advances per replay as _ppo_epoch_fused advances it."""
+        N = recs.shape[0]
+        spans = [(s, min(N, s + self.chunk)) for s in range(0, N, self.chunk)]
+        if self._ubufs is None or self._ubufs["N"] != N:
+            kw = dict(device=self.dev)
+            self._ubufs = {"N": N, "chunks": []}
+            for s, e in spans:
+                m = e - s
+                self._ubufs["chunks"].append({
+                    "rows": (torch.empty(m, 64, dtype=torch.uint8, **kw), torch.empty(m, dtype=torch.int32, **kw),
+                             torch.empty(m, dtype=torch.float32, **kw), torch.empty(m, dtype=torch.float32, **kw),
+                             torch.empty(m, dtype=torch.float32, **kw)),
+                    "plan": (torch.empty(m, dtype=torch.int32, **kw), torch.empty(33, dtype=torch.int32, **kw),
+                             torch.empty(8, dtype=torch.int32, **kw))})
+            self._ugraph = None
+        for (s, e), c in zip(spans, self._ubufs["chunks"]):
+            perm, _, _ = ppo_row_plan(recs[s:e], self.A, out=c["plan"])
+            gather_rollout(perm, recs[s:e], acts[s:e], old[s:e], R[s:e], adv[s:e], out=c["rows"])
+
+        def chunks():
+            for c in self._ubufs["chunks"]:
+                rr, aa, oo, RR, dd = c["rows"]
+                _, plan, row_plan = c["plan"]
+                yield None, None, aa, oo, RR, dd, rr, {"plan": (None, plan, row_plan)}
+
+        parts = None
+        cur = torch.cuda.current_stream(self.dev)
+        for _ in range(NUM_EPOCHS):
+            key = (hint["scale"], float(self.entropy_coef), N)
+            if self._ugraph is None or self._ugraph[0] != key:
+                self._ugraph = None
+                st = torch.cuda.Stream(self.dev)
+                st.wait_stream(cur)
+                out = {}
+
+                def body():
+                    out["e"] = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
+                                         amp=self.amp, fused=self.fused, sync=False, guard=guard, fused_head=True,
+                                         scale_hint=dict(hint))
+                g = capture("ppo_update", body, st)
+                cur.wait_stream(st)
+                self._ugraph = (key, g, out["e"])
+            self._ugraph[1].replay()
+            e = self._ugraph[2]
+            parts = e.clone() if parts is None else parts + e
+            if self.scaler.is_enabled():         # as _ppo_epoch_fused advances its scale_hint
+                t = hint["tracker"] + 1
+                if t == self.scaler._growth_interval:
+                    hint["scale"] = float(np.float32(hint["scale"] * self.scaler._growth_factor))
+                    t = 0
+                hint["tracker"] = t
         return parts
 
     def _snapshot_tensors(self):

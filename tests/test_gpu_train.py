@@ -373,3 +373,30 @@ def test_update_redone_after_skipped_step(monkeypatch):
     assert sa == sb == 32768.0
     for a, b in zip(pa + ma, pb + mb):
         assert torch.allclose(a, b, rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("growth_interval", [2000, 3])
+def test_update_graphs_match_eager(growth_interval):
+    """The update's fused-head epoch replayed as a HIP graph (captured at the second
+    update over persistent row buffers, recaptured when the GradScaler scale grows)
+    gives bit-identical weights, Adam state, scale and loss parts to the eager epochs,
+    update after update.  growth_interval 3: the scale grows inside an update, so the
+    graph is recaptured between two of its epochs."""
+    from bgx.train import PPOTrainer
+    trs = [PPOTrainer(batch=8192, horizon=4, seed=21, update_graphs=g) for g in (False, True)]
+    for tr in trs:
+        tr.scaler._growth_interval = growth_interval
+    for it in range(3):
+        ms = []
+        for tr in trs:
+            tr.rollout()
+            ms.append(tr.update())
+        torch.cuda.synchronize()
+        assert (trs[1]._ugraph is not None) == (it >= 1) and trs[0]._ugraph is None
+        for a, b in zip(trs[0].net.parameters(), trs[1].net.parameters()):
+            assert torch.equal(a, b), it
+        for a, b in zip(trs[0].net.parameters(), trs[1].net.parameters()):
+            assert torch.equal(trs[0].opt.state[a]["exp_avg_sq"], trs[1].opt.state[b]["exp_avg_sq"]), it
+        assert float(trs[0].scaler._scale.item()) == float(trs[1].scaler._scale.item())
+        # loss parts: fp64 sums of per-workgroup partials in atomic order
+        assert all(ms[0][k] == pytest.approx(ms[1][k], rel=1e-12, abs=1e-12) for k in ms[0]), it
