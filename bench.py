@@ -667,6 +667,7 @@ def main():
     else:
         for _ in range(args.steps):
             step(True)
+    t_enq = time.perf_counter() - t0             # host time to enqueue the timed steps
     torch.cuda.synchronize(dev)
     barrier(ws)
     torch.cuda.synchronize(dev)
@@ -752,6 +753,7 @@ def main():
     line["roofline"]["chip_wide"] = {"achieved": chip, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": chip / HBM_PEAK_GBS, "algorithmic_bytes_per_step": B * bytes_per_lane,
                                      "window_ms": ms_step, "note": "all shards' algorithmic env-step bytes / ms_per_step"}
+    line["host_enqueue_ms"] = t_enq * 1e3
     line["per_rank"] = [{"rank": k, "env_steps": r[0], "seconds": r[1]} for k, r in enumerate(per_rank)]
     if backend is not None:
         line["dist_backend"] = backend

@@ -60,11 +60,7 @@ __device__ unsigned long long g_scnt[16];
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-#ifdef BGX_PAIR_1WAVE
-constexpr int kEvalWideWaves = 4, kEvalNarrowWaves = 4;   // experiment: one wave per SIMD at H = 128
-#else
 constexpr int kEvalWideWaves = 8, kEvalNarrowWaves = 4;   // waves per LDS-weight evaluator workgroup
-#endif   // waves per LDS-weight evaluator workgroup
 constexpr int kKB = 13;            // 208 / 16 k-steps of v_mfma_f32_32x32x16_f16
 constexpr int kSlowQueue = 1 << 20;
 constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
@@ -790,8 +786,8 @@ __device__ __forceinline__ uint32_t f16_pair(uint32_t ab, float s0, float s1) {
 // builtins (round 5): hipcc folds min(max(x, 0), 1) into the VOP3P clamp bit, so this is
 // the same five instructions (3 v_pk_add_f16 clamp, v_pk_fma_f16, v_pk_max_f16) as the
 // round-3/4 inline-asm block, and the hazard recognizer now sees every one of them (the
-// asm string hid them; it was not the cause of the two-tiles-in-flight fault, which the
-// builtin form shows as well: eval_tile_wide).
+// asm string hid them; it was not the cause of the two-tiles-in-flight fault: see
+// eval_tile_wide).
 __device__ __forceinline__ h16x2 clamp01h(h16x2 x) {
     return __builtin_elementwise_min(__builtin_elementwise_max(x, (h16x2){0, 0}), (h16x2){1, 1});
 }
@@ -857,14 +853,14 @@ __device__ __forceinline__ float unord_f32(int i) { return __int_as_float(i >= 0
 // asm would hide the MFMA-result read from the hazard recognizer, which must pad it)
 __device__ __forceinline__ float relu_raw(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
-// Wide tiles (H > 64), one leaf tile of 32 columns at a time.  Two leaf tiles in flight
-// (sharing each weight fragment, 128 accumulator VGPRs at H = 128; -DBGX_WIDE_PAIR builds
-// that form for experiments) give wrong values in columns 16-31 of the second tile for a
-// few leaves, varying with the build's instruction layout -- with the feature units as
-// inline asm (rounds 3-4) and as builtins (round 5) alike, with no EXEC-masked MFMA, no
-// MFMA whose D differs from its C, and every MFMA-result read >= 12 wait states after its
-// producer in the ISA.  One tile at a time is exact on every leaf
-// (test_two_ply_every_leaf_vs_fp64: all 534 k leaves of a 48-root batch against fp64).
+// Wide tiles (H > 64) in the unfactored form (no row parts), one leaf tile of 32 columns
+// at a time.  The factored form (eval_leaves_fact, the C4 path) keeps two leaf tiles in
+// flight.  Round 4's wrong values with two tiles in flight (columns 16-31 of one tile,
+// 0.01-0.1 % of leaves, varying from run to run) came from packed-fp32 FMAs that LLVM's
+// SLP vectorizer formed across the two tiles' value heads (v_pk_fma_f32 broadcasting the
+// odd head weights with op_sel:[0,1,0], an instruction form no other kernel here uses);
+// bg_search.hip is built without SLP vectorization (__graft_entry__.SOURCE_FLAGS) and the
+// two-tile form is exact on every leaf.
 template <int NT>
 __device__ __forceinline__ float eval_tile_wide(const uint4* wq, const float* wvs, const Leaf& L, int z, float bias) {
     constexpr int NW = slices(NT) / 2;
@@ -1014,11 +1010,7 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
     // narrow: the row parts are loaded first and added after the MFMAs (their latency hidden
     // behind them; 15.9 vs 31.5 ms per C4 batch at H = 40); wide: they start the accumulators
     // (30.6 vs 31.4 ms at H = 128)
-#ifdef BGX_PAIR_LATE
-    constexpr bool kLate = true;
-#else
     constexpr bool kLate = !kWide;
-#endif
     float4 rpv[NN][NA][kWide ? 4 : 2];
     if constexpr (kLate) {
     #pragma unroll
@@ -1055,18 +1047,10 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
             if constexpr (kWide) {
                 const f16x8 ah = __builtin_bit_cast(f16x8, wq[((kb * NA + t) * 2 + 0) * 64 + l + z]);
                 const f16x8 al = __builtin_bit_cast(f16x8, wq[((kb * NA + t) * 2 + 1) * 64 + l + z]);
-#ifdef BGX_PAIR_NOP
-                __builtin_amdgcn_sched_barrier(0);
-                __asm__ volatile("s_nop 4" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-#endif
                 #pragma unroll
                 for (int n = 0; n < NN; ++n) {
                     x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, f[n], first ? (f32x16){} : x[n][t], 0, 0, 0);
                     x[n][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, f[n], x[n][t], 0, 0, 0);
-#ifdef BGX_PAIR_SPLIT
-                    __builtin_amdgcn_sched_barrier(0);
-#endif
                 }
             } else {
                 const f16x8 a = __builtin_bit_cast(f16x8, wq[(kb * NT + t) * 64 + l + z]);
@@ -1104,11 +1088,6 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
         for (int n = 0; n < NN; ++n) f[n] = hit_delta(L[n].hits, k6, h);
         block(6 * P + k6, f, false);
     }
-#ifdef BGX_EVAL_PAD
-    __builtin_amdgcn_sched_barrier(0);
-    __asm__ volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#endif
     if constexpr (kLate)
     #pragma unroll
     for (int n = 0; n < NN; ++n)
@@ -1254,15 +1233,24 @@ void k_eval(EvalArgs E) {
     LeafRow row[2];
     #pragma unroll
     for (int n = 0; n < 2; ++n) { raw[n] = load_raw(E, tile * 64 + 32 * n + c); row[n] = load_row(E, raw[n]); }
+    // the next tile's pool entries are loaded behind the current tile's MFMAs, except at
+    // H = 128 (two leaf tiles' 128 accumulators: the prefetch registers would spill)
+    constexpr bool kPrefetch = !wide_tiles(NT);
     for (; tile < tiles; tile += stride) {
         Leaf L[2];
+        if constexpr (!kPrefetch) {
+            #pragma unroll
+            for (int n = 0; n < 2; ++n) { raw[n] = load_raw(E, tile * 64 + 32 * n + c); row[n] = load_row(E, raw[n]); }
+        }
         #pragma unroll
         for (int n = 0; n < 2; ++n) L[n] = make_leaf(raw[n], row[n]);
         int z = 0;
         __asm__ volatile("" : "+s"(z));
-        const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
-        #pragma unroll
-        for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
+        if constexpr (kPrefetch) {
+            const unsigned long long nxt = tile + stride < tiles ? tile + stride : tile;
+            #pragma unroll
+            for (int n = 0; n < 2; ++n) raw[n] = load_raw(E, nxt * 64 + 32 * n + c);
+        }
         float v[2];
         if (E.rowpart) {
             // the factored form once per replier among the pair's valid leaves (wave-uniform;
@@ -1276,8 +1264,8 @@ void k_eval(EvalArgs E) {
                 float w[2];
                 int zq = z;                               // opaque per pass: no LDS read hoisted out
                 __asm__ volatile("" : "+s"(zq));
-#ifndef BGX_WIDE_PAIR
-                if constexpr (wide_tiles(NT)) {         // one leaf tile at a time (eval_tile_wide)
+#ifdef BGX_WIDE_SINGLE
+                if constexpr (wide_tiles(NT)) {         // experiment: one leaf tile at a time
                     eval_leaves_fact<NT, 1>(wq, wvs, &F[0], zq, E.bv, E.rowpart, qq, &w[0]);
                     __builtin_amdgcn_sched_barrier(0);
                     int zr = zq;
@@ -1294,9 +1282,9 @@ void k_eval(EvalArgs E) {
         } else {
             eval_leaves<NT>(wq, wvs, L, z, E.bv, v);
         }
-        #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-            row[n] = load_row(E, raw[n]);
+        if constexpr (kPrefetch) {
+            #pragma unroll
+            for (int n = 0; n < 2; ++n) row[n] = load_row(E, raw[n]);
         }
         if (E.vdbg && h == 0) {
             E.vdbg[tile * 64 + c] = v[0];

@@ -50,7 +50,7 @@ def test_library_built_from_these_sources():
     import bgx._lib as L
     if not os.path.exists(L.LIB_PATH):
         pytest.skip("libbgx.so not built")
-    want = L.source_hash(" ".join(G.HIPCC_FLAGS))
+    want = L.source_hash(G.flags_id())
     assert L.embedded_build_id() == want
     assert L.load().bgx_build_id().decode() == want
 

@@ -36,14 +36,13 @@ NAMES = {1: "nd_rows", 3: "nd_rows_rejected", 4: "slow_rolls_in_fast_rows", 5: "
 def build():
     sys.path.insert(0, ROOT)
     import __graft_entry__ as G
-    flags = [f for f in G.HIPCC_FLAGS if f != "-shared"] + ["-DBGX_COUNTERS"]
     with tempfile.TemporaryDirectory() as tmp:
         objs = []
         procs = []
         for s in G.HIP_SOURCES:
             o = os.path.join(tmp, s + ".o")
             objs.append(o)
-            procs.append(subprocess.Popen(["hipcc"] + flags + ["-I" + os.path.join(ROOT, "include"), "-c",
+            procs.append(subprocess.Popen(["hipcc"] + G.hipcc_flags(s) + ["-DBGX_COUNTERS", "-I" + os.path.join(ROOT, "include"), "-c",
                                                               os.path.join(PKG, "csrc", s), "-o", o]))
         if any(p.wait() for p in procs):
             raise SystemExit("hipcc failed")
