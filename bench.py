@@ -214,7 +214,8 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4, stre
     `streams`: the C3 leg's shard streams, reused when the shard counts match."""
     from bgx.train import PPOTrainer
     group = None
-    tr = PPOTrainer(batch=B, horizon=horizon, seed=11, device=dev, process_group=group, streams=streams)
+    kw = {"chunk": int(os.environ["BGX_PPO_CHUNK"])} if os.environ.get("BGX_PPO_CHUNK") else {}
+    tr = PPOTrainer(batch=B, horizon=horizon, seed=11, device=dev, process_group=group, streams=streams, **kw)
     tr.iteration()                                   # warm
     torch.cuda.synchronize(dev)
     barrier(ws)

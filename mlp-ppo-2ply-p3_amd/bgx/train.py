@@ -613,7 +613,7 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
 class PPOTrainer:
     def __init__(self, batch: int = 65536, horizon: int = 64, hidden: int = 128, n_actions: int = 500,
                  seed: int = 0, device=None, process_group=None, pinned: bool = False, returns: str = "lane",
-                 chunk: int = 1 << 20, fused: bool | None = None, amp: bool = True,
+                 chunk: int = 1 << 21, fused: bool | None = None, amp: bool = True,
                  entropy_anneal: str = "train", shards: int | None = None, graphs: bool | None = None,
                  fork: bool | None = None, streams=None, update_graphs: bool | None = None):
         if entropy_anneal not in ("train", "train_single"):
@@ -624,6 +624,9 @@ class PPOTrainer:
         self.rank = dist.get_rank(process_group) if _world(process_group) > 1 else 0
         self.B, self.T, self.A = batch, horizon, n_actions
         self.returns_mode = returns
+        # rows per update chunk (gradient accumulation over chunks): 2^21 = a whole 65,536 x 32
+        # rollout in one chunk, the reference's single full batch; 2^20-row chunks cost
+        # 8.4 vs 7.8 ms per update (twice the per-call partial sums and launches)
         self.chunk = chunk
         self.fused = (self.dev.type == "cuda") if fused is None else fused
         self.amp = amp            # the reference's autocast (fp16 on the GPU); False = fp32 update
