@@ -242,13 +242,17 @@ def ppo_iteration_bench(B: int, horizon: int, ws: int, dev, iters: int = 4, stre
     return out
 
 
-def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 4, graphs: bool = True):
+def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: int = 4, graphs: bool = True,
+                           streams=None):
     """C2: B games per GPU, greedy 1-ply self-play with the value head
     MLP(198->40->1): every step = V over each lane's legal afterstates (mover's
     one-hot, as legal_board_features) -> first argmax -> env.step.  The B games
     run as `shards` engines on their own streams: at this batch each launch is
     bound by its slowest lane, so one shard's search runs beside the other's
-    step."""
+    step.  `streams`: the C3 leg's shard streams (one hardware queue each), reused
+    when the shard counts match: fresh pool streams can share a hardware queue (HIP
+    maps streams to its 4 queues round-robin as they are created), which serialised
+    two shards (31 vs 52 M env steps/s once the C4 leg had taken pool streams)."""
     import bgx
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead, one_ply
@@ -257,7 +261,8 @@ def one_ply_selfplay_bench(B: int, steps: int, ws: int, rank: int, dev, shards: 
     S = shards if B % shards == 0 else 1
     engs = [bgx.Engine(batch=B // S, max_moves=500, seed=123 + rank + 7919 * k, dice="philox", auto_reset=True,
                        device=dev) for k in range(S)]
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    if streams is None or len(streams) != S:
+        streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     for e in engs:
         e.reset(want_obs=False)
         e.set_fork(False)          # one stream per step: 43.1 vs 38.9 M forked (profiles/r4_layout/r4o)
@@ -340,13 +345,14 @@ def two_ply_shards(eng, shards: int):
     return out
 
 
-def two_ply_bench(engs, batches: int, ws: int, dev, hidden: int = 40):
+def two_ply_bench(engs, batches: int, ws: int, dev, hidden: int = 40, streams=None):
     """C4: 2-ply expectimax over the 21 rolls for every lane's current position
     (B roots per GPU), value head MLP(198->H->1) on MFMA.  The roots run
     as len(engs) game shards, each on its own stream driven by its own host thread (a
     bgx_two_ply call synchronises its stream after the row scan and after the pool
     pass; ctypes drops the GIL inside it), so one shard's reply enumeration runs beside
-    another's evaluation.  Shard k > 0 starts k/S of a batch later."""
+    another's evaluation.  Shard k > 0 starts k/S of a batch later.  `streams`: the C3
+    leg's shard streams (one hardware queue each), reused when the counts match."""
     import threading
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead, two_ply, two_ply_timings
@@ -354,7 +360,8 @@ def two_ply_bench(engs, batches: int, ws: int, dev, hidden: int = 40):
     vnet = PolicyNet(hidden_size=hidden).to(dev)
     vh = ValueHead(vnet)
     S = len(engs)
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    if streams is None or len(streams) != S:
+        streams = [torch.cuda.Stream(dev) for _ in range(S)]
     for st in streams:
         st.wait_stream(torch.cuda.current_stream(dev))
     t_warm = 0.0
@@ -854,11 +861,20 @@ def main():
                 a2, _, _ = net.act(eng2, seed=5, step=i)
                 eng2.step(a2, want_obs=False, want_info=False)
         c4 = two_ply_shards(eng2, args.c4_shards)
-        line["two_ply"] = two_ply_bench(c4, args.two_ply_batches, ws, dev)
+        line["two_ply"] = two_ply_bench(c4, args.two_ply_batches, ws, dev, streams=streams)
+        if len(c4) > 1:
+            # the evaluator's roofline from one whole-batch engine (its HIP-event phases are
+            # not shared with another shard's enumeration); the shards' own per-shard figure,
+            # taken while the other shards' kernels share the GPU, is kept beside it
+            one = two_ply_bench([eng2], 1, ws, dev, streams=streams[:1])
+            line["two_ply"]["roofline_per_shard_overlapped"] = line["two_ply"]["roofline"]
+            line["two_ply"]["roofline"] = dict(one["roofline"], source="one engine of all B roots, 1 batch")
+            line["two_ply"]["one_engine"] = {k: one[k] for k in ("root_decisions_per_s", "enumeration_ms_per_batch",
+                                                                "evaluation_ms_per_batch", "leaves_per_root")}
         del c4
         # the same roots with the reference's H = 128 value head (agent/config.py:8)
         # (one engine: its phase times are those of a whole B-root batch)
-        line["two_ply_h128"] = two_ply_bench([eng2], 1, ws, dev, hidden=128)
+        line["two_ply_h128"] = two_ply_bench([eng2], 1, ws, dev, hidden=128, streams=streams[:1])
         enums = (summ or {}).get("two_ply_enum") if prof_ok else None
         if enums:
             # tools/profile.sh's enum passes run --two-ply-batches 1: a warm and a timed batch
@@ -876,7 +892,7 @@ def main():
             torch.cuda.empty_cache()
     if args.c2_steps > 0:
         line["one_ply_selfplay"] = one_ply_selfplay_bench(4096, args.c2_steps, ws, rank, dev, args.c2_shards,
-                                                          not args.no_graphs)
+                                                          not args.no_graphs, streams=streams)
     if args.horizon > 0 and args.workload in ("c3", "ppo"):
         # the trainer's shards on the C3 leg's streams (one hardware queue each)
         tr_shards = 4 if B >= 65536 and B % 1024 == 0 else (2 if B >= 32768 and B % 256 == 0 else 1)
