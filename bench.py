@@ -351,8 +351,9 @@ def two_ply_bench(engs, batches: int, ws: int, dev, hidden: int = 40, streams=No
     as len(engs) game shards, each on its own stream driven by its own host thread (a
     bgx_two_ply call synchronises its stream after the row scan and after the pool
     pass; ctypes drops the GIL inside it), so one shard's reply enumeration runs beside
-    another's evaluation.  Shard k > 0 starts k/S of a batch later.  `streams`: the C3
-    leg's shard streams (one hardware queue each), reused when the counts match."""
+    another's evaluation.  Shard k > 0 starts k/S of a batch later.  `streams`: given
+    streams instead of fresh pool streams (the bench passes none: the C3 leg's streams
+    gave 1.73-1.80 M against 1.80-1.84 M on fresh ones)."""
     import threading
     from bgx.policy import PolicyNet
     from bgx.search import ValueHead, two_ply, two_ply_timings
@@ -861,12 +862,12 @@ def main():
                 a2, _, _ = net.act(eng2, seed=5, step=i)
                 eng2.step(a2, want_obs=False, want_info=False)
         c4 = two_ply_shards(eng2, args.c4_shards)
-        line["two_ply"] = two_ply_bench(c4, args.two_ply_batches, ws, dev, streams=streams)
+        line["two_ply"] = two_ply_bench(c4, args.two_ply_batches, ws, dev)
         if len(c4) > 1:
             # the evaluator's roofline from one whole-batch engine (its HIP-event phases are
             # not shared with another shard's enumeration); the shards' own per-shard figure,
             # taken while the other shards' kernels share the GPU, is kept beside it
-            one = two_ply_bench([eng2], 1, ws, dev, streams=streams[:1])
+            one = two_ply_bench([eng2], 1, ws, dev)
             line["two_ply"]["roofline_per_shard_overlapped"] = line["two_ply"]["roofline"]
             line["two_ply"]["roofline"] = dict(one["roofline"], source="one engine of all B roots, 1 batch")
             line["two_ply"]["one_engine"] = {k: one[k] for k in ("root_decisions_per_s", "enumeration_ms_per_batch",
@@ -874,7 +875,7 @@ def main():
         del c4
         # the same roots with the reference's H = 128 value head (agent/config.py:8)
         # (one engine: its phase times are those of a whole B-root batch)
-        line["two_ply_h128"] = two_ply_bench([eng2], 1, ws, dev, hidden=128, streams=streams[:1])
+        line["two_ply_h128"] = two_ply_bench([eng2], 1, ws, dev, hidden=128)
         enums = (summ or {}).get("two_ply_enum") if prof_ok else None
         if enums:
             # tools/profile.sh's enum passes run --two-ply-batches 1: a warm and a timed batch
