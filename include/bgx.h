@@ -340,8 +340,9 @@ int bgx_fc1_records_ex(const uint8_t* records_dev, int32_t n, const void* packed
  * persistent grids of 4 workgroups per CU (1 for the 16-tile variant).
  * bgx_ppo_gw2: gw2 [512][128] += dy^T h and gb2 [512] += column sums of dy (fp32),
  * dy recomputed from the statistics; plan int32[33] = task prefix per action tile
- * (17 entries, tasks of BGX_PPO_GW2_TASK_TILES row tiles) then the first row tile
- * (of perm order) each action tile needs (16); workspace of
+ * (17 entries; the tasks of action tile o are the groups of BGX_PPO_GW2_TASK_TILES
+ * row tiles, aligned at multiples of it, that hold a row tile >= its start) then the
+ * first row tile (of perm order) each action tile needs (16); workspace of
  * bgx_ppo_gw2_workspace(m) bytes. */
 #define BGX_PPO_GW2_TASK_TILES 32
 int bgx_ppo_rows(const void* h_dev, const int32_t* perm_dev, const uint8_t* records_dev, const int32_t* actions_dev,

@@ -388,7 +388,9 @@ def ppo_row_plan_torch(records: torch.Tensor, n_actions: int = 500):
     start = torch.div(cum[:16], 32, rounding_mode="floor")
     start[15] = 0                                     # the value column's tile: every row
     ntiles = (m + 31) // 32
-    tasks = (ntiles - start + PPO_GW2_TASK_TILES - 1) // PPO_GW2_TASK_TILES
+    # tasks of tile o: the kTS-aligned row groups that hold a row tile >= start[o]
+    tasks = (ntiles + PPO_GW2_TASK_TILES - 1) // PPO_GW2_TASK_TILES - torch.div(start, PPO_GW2_TASK_TILES,
+                                                                                rounding_mode="floor")
     pre = torch.cat([torch.zeros(1, dtype=tasks.dtype, device=tasks.device), torch.cumsum(tasks, 0)])
     # row tiles whose last (largest) row needs <= k tiles: cum[k] // 32, all of them at cum[k] == m
     e = torch.where(cum[[1, 2, 4]] >= m, torch.full_like(cum[[1, 2, 4]], ntiles), cum[[1, 2, 4]] // 32)

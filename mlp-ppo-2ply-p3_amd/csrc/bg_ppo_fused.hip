@@ -467,14 +467,45 @@ __global__ __launch_bounds__(256) void k_ppo_gw2(Gw2Args a) {
     __shared__ int32_t sinf[4][32];
     const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int r = l & 31, hh = l >> 5;
-    const int task = blockIdx.x * 4 + wv;
-    if (task >= a.plan[kNT]) return;                                        // whole waves only
-    int at = 0;
-    #pragma unroll
-    for (int b = 1; b < kNT; ++b) at = a.plan[b] <= task ? b : at;
+    const int t = blockIdx.x * 4 + wv;                                      // launch order
+    if (t >= a.plan[kNT]) return;                                           // whole waves only
+    // Launch order = row group major: the tasks of one group of kTS row tiles (one per
+    // action tile its rows reach) are consecutive, so the waves reading the same h rows
+    // run together on one CU and all but the first read them from the L2 (action-tile
+    // major, each h row came from HBM once per action tile: ~2.5x).  Group g reaches
+    // action tile o iff f_o = start(o) / kTS <= g; P(g) = tasks of the groups before g
+    // = sum_o max(0, g - f_o).  A task's partial keeps its action-tile-major slot
+    // plan[o] + (g - f_o), so the fixed-order sums see the same layout.
     const int ntiles = (a.m + 31) >> 5;
-    const int tile0 = a.plan[17 + at] + (task - a.plan[at]) * kTS;
-    const int tile1 = min(tile0 + kTS, ntiles);
+    const int ngroups = (ntiles + kTS - 1) / kTS;
+    int f[kNT];
+    #pragma unroll
+    for (int o = 0; o < kNT; ++o) f[o] = a.plan[17 + o] / kTS;
+    auto prefix = [&](int g) {
+        int p = 0;
+        #pragma unroll
+        for (int o = 0; o < kNT; ++o) p += max(0, g - f[o]);
+        return p;
+    };
+    int lo = 0, hi = ngroups;                                               // largest g with P(g) <= t
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (prefix(mid) <= t) lo = mid; else hi = mid;
+    }
+    const int g = lo;
+    int j = t - prefix(g), at = 0;
+    #pragma unroll
+    for (int o = kNT - 1; o >= 0; --o) {                                     // the j-th o with f_o <= g
+        if (f[o] <= g) {
+            int before = 0;
+            #pragma unroll
+            for (int q = 0; q < kNT; ++q) before += (q < o && f[q] <= g) ? 1 : 0;
+            if (before == j) at = o;
+        }
+    }
+    const int task = a.plan[at] + (g - f[at]);                              // the partial's slot
+    const int tile0 = max(g * kTS, a.plan[17 + at]);
+    const int tile1 = min((g + 1) * kTS, ntiles);
     uint4 bw[8];                                                            // B operand: W2h[32at + r][16s + 8hh + j]
     const uint4* wp = (const uint4*)(a.w2h + (size_t)(32 * at + r) * kH);
     #pragma unroll
@@ -913,7 +944,7 @@ __global__ __launch_bounds__(1024) void k_plan_scan(const int32_t* __restrict__ 
             const int st = o == 15 ? 0 : cum[o] / 32;
             plan[17 + o] = st;
             plan[o] = pre;
-            pre += (ntiles - st + kTS - 1) / kTS;
+            pre += (ntiles + kTS - 1) / kTS - st / kTS;          // kTS-aligned row groups from st
         }
         plan[16] = pre;
         int e[3];
