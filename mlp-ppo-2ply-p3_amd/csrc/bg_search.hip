@@ -63,7 +63,15 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr int kEvalWideWaves = 8, kEvalNarrowWaves = 4;   // waves per LDS-weight evaluator workgroup
 constexpr int kKB = 13;            // 208 / 16 k-steps of v_mfma_f32_32x32x16_f16
 constexpr int kSlowQueue = 1 << 20;
-constexpr int kBlk = 256;          // leaf-pool allocation block (slots)
+// Leaf-pool allocation block (slots): a wave claims kBlk slots with one atomic on the
+// pool's single cursor.  That cursor is one address hit from all eight XCDs: at 256 slots
+// (1.9 M claims per 65,536-root batch) the claims serialised the enumerators (23.7 ms
+// per batch; 1,024: 19.0 ms; 4,096: 19.1 ms with 0.4 ms more evaluation of the wasted
+// tails; profiles/r5/pool_block/)
+#ifndef BGX_POOL_BLK
+#define BGX_POOL_BLK 1024
+#endif
+constexpr int kBlk = BGX_POOL_BLK;
 constexpr uint32_t kTagNone = 0xFFFFFFFFu;
 constexpr int kLogLight = 8;       // non-doubles reply enumeration: 256-slot table (4 KiB)
 constexpr int kMaxRounds = 256;
