@@ -663,6 +663,9 @@ constexpr int kW1 = 208;                    // gw1 row width (198 features, ones
 constexpr int kGw1Part = kFB * 32 * kH;     // floats per workgroup partial, [224][128]
 constexpr int kGw1Grid = 512;               // workgroups (2 per CU)
 constexpr int kGw1Rows = 64;                // rows per LDS stage: two 32-row MFMA tiles per barrier
+                                            // (32 rows: the same time; 128: registers spill, 2x slower)
+constexpr int kGw1Dh = kGw1Rows * 16 / 512; // 16-byte dh chunks per thread and stage
+constexpr int kGw1RecThreads = kGw1Rows / 4 * 14;     // record loaders: 4 rows x one dword each
 
 // Every feature but off / 15 is exact in f16 arithmetic on t = 1024 + v (f16 has unit
 // spacing at 1024): u = min(max(t A + B, 0), C) with n >= k: (1, -1024 - k, 1);
@@ -717,6 +720,13 @@ struct Gw1Args {
     float* part;                // [grid][224][128]
 };
 
+// The transposed records [byte][row]: byte b of row r at b * kGw1Rows + ((r + 4 (b >> 2)) mod
+// kGw1Rows), a rotation by the byte's dword so that the 14 lanes storing one row group's 14
+// dwords hit 14 banks; 4 consecutive rows r = 0 mod 4 stay one aligned dword, stored whole.
+// (Round 4 stored single bytes, all 56 lanes of a row-major mapping on one bank: 90 of the
+// kernel's 342 us per 2^21 rows.)
+__device__ __forceinline__ int srt_at(int b, int r) { return b * kGw1Rows + ((r + 4 * (b >> 2)) & (kGw1Rows - 1)); }
+
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k_ppo_gw1(Gw1Args a) {
     __shared__ __attribute__((aligned(16))) uint8_t sdh[2][kGw1Rows * 256];
     __shared__ __attribute__((aligned(16))) uint8_t srt[2][56 * kGw1Rows];
@@ -738,51 +748,61 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     // (bytes 0..55): dwords tid and, for tid < 384, tid + 512.  Two stages in flight: the
     // loads of stage t + 2 are issued while stage t is computed.
     const uint4 z4 = make_uint4(0, 0, 0, 0);
-    struct Ld { uint4 d[2]; uint32_t rw[2]; };
+    // records: thread t < kGw1RecThreads loads dword dw = t % 14 of rows 4g..4g+3, g = t / 14
+    // (lanes of one row group read one row's 56 bytes contiguously per load) and stores the
+    // four transposed dwords (byte 4dw + q of the 4 rows) whole
+    struct Ld { uint4 d[kGw1Dh]; uint32_t rw[4]; };
+    const int rg = tid / 14, rdw = tid - 14 * rg;
     auto load = [&](int st) {
-        Ld x{{z4, z4}, {0u, 0u}};
+        Ld x;
+        #pragma unroll
+        for (int k = 0; k < kGw1Dh; ++k) x.d[k] = z4;
+        #pragma unroll
+        for (int j = 0; j < 4; ++j) x.rw[j] = 0u;
         if (st >= t1) return x;
         const int row0 = st * kGw1Rows;
         #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kGw1Dh; ++k) {
             const int c = tid + 512 * k;
             x.d[k] = row0 + (c >> 4) < a.m ? ((const uint4*)(a.dh + (size_t)(row0 + (c >> 4)) * kH))[c & 15] : z4;
         }
-        #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int w = tid + 512 * k, r = w / 14, dw = w - 14 * r;
-            if (k == 0 || tid < 384) {
-                const int gr = row0 + r < a.m ? row0 + r : a.m - 1;
-                x.rw[k] = ((const uint32_t*)(a.rec + (size_t)gr * 64))[dw];
+        if (tid < kGw1RecThreads)
+            #pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int r = row0 + 4 * rg + j, gr = r < a.m ? r : a.m - 1;
+                x.rw[j] = ((const uint32_t*)(a.rec + (size_t)gr * 64))[rdw];
             }
-        }
         return x;
     };
     Ld q0 = load(t0), q1 = load(t0 + 1);
     int buf = 0;
     for (int st = t0; st < t1; ++st, buf ^= 1) {
         #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kGw1Dh; ++k) {
             const int c = tid + 512 * k;
             *(uint4*)(sdh[buf] + swz(c >> 4, c & 15)) = q0.d[k];
         }
-        #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int w = tid + 512 * k, r = w / 14, dw = w - 14 * r;
-            if (k == 0 || tid < 384)
-                #pragma unroll
-                for (int q = 0; q < 4; ++q) srt[buf][(4 * dw + q) * kGw1Rows + r] = (uint8_t)(q0.rw[k] >> (8 * q));
-        }
+        if (tid < kGw1RecThreads)
+            #pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t v = ((q0.rw[0] >> (8 * q)) & 255u) | (((q0.rw[1] >> (8 * q)) & 255u) << 8) |
+                                   (((q0.rw[2] >> (8 * q)) & 255u) << 16) | (((q0.rw[3] >> (8 * q)) & 255u) << 24);
+                *(uint32_t*)(srt[buf] + srt_at(4 * rdw + q, 4 * rg)) = v;
+            }
         __syncthreads();
         q0 = q1;
         q1 = load(st + 2);                                  // behind this stage's MFMAs
         if (fb == kFB) continue;                            // the loader wave (wave-uniform)
         #pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
+        for (int sub = 0; sub < kGw1Rows / 32; ++sub)
             #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
-                const uint8_t* bp = srt[buf] + byte * kGw1Rows + 32 * sub + 16 * s2 + 4 * hh;
-                const f16x8 A = gw1_feats(*(const uint32_t*)bp, *(const uint32_t*)(bp + 8), fa, fbv, fc, off);
+                int rr = 4 * (byte >> 2) + 4 * hh;          // laundered: recomputed per use, not
+                __asm__ volatile("" : "+v"(rr));            // hoisted into 8 registers
+                const uint8_t* bp = srt[buf] + byte * kGw1Rows;
+                const f16x8 A = gw1_feats(*(const uint32_t*)(bp + ((rr + 32 * sub + 16 * s2) & (kGw1Rows - 1))),
+                                          *(const uint32_t*)(bp + ((rr + 32 * sub + 16 * s2 + 8) & (kGw1Rows - 1))),
+                                          fa, fbv, fc, off);
                 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
