@@ -23,8 +23,12 @@ namespace bg {
 
 // Work counters for experiments (built with -DBGX_COUNTERS only).
 #ifdef BGX_COUNTERS
-__device__ unsigned long long g_cnt[16];
-#define BG_CNT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&bg::g_cnt[i], (unsigned long long)(v)); } while (0)
+// each counter spread over kCntSlots addresses (by workgroup): one address hit by every
+// wave of the chip serialises the atomics and distorts the timings being measured
+constexpr int kCntSlots = 1024;
+__device__ unsigned long long g_cnt[16 * kCntSlots];
+#define BG_CNT(i, v) do { if ((threadIdx.x & 63) == 0) \
+    atomicAdd(&bg::g_cnt[(i) * bg::kCntSlots + (blockIdx.x & (bg::kCntSlots - 1))], (unsigned long long)(v)); } while (0)
 #define BG_T0(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define BG_T1(i, t) BG_CNT(i, __builtin_amdgcn_s_memtime() - t)
 #else

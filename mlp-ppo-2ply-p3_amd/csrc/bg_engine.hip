@@ -694,9 +694,14 @@ int bgx_engine_mt_state(bgx_engine* e, int32_t lane, uint32_t* state_host, int32
 #ifdef BGX_COUNTERS
 extern "C" int bgx_debug_counters(unsigned long long* out16) {
     CK(hipDeviceSynchronize());
-    CK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bg::g_cnt), 16 * 8));
-    unsigned long long z[16] = {0};
-    CK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z, 16 * 8));
+    constexpr size_t n = 16 * (size_t)bg::kCntSlots;
+    std::vector<unsigned long long> h(n), z(n, 0ull);
+    CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(bg::g_cnt), n * 8));
+    for (int i = 0; i < 16; ++i) {
+        out16[i] = 0;
+        for (int k = 0; k < bg::kCntSlots; ++k) out16[i] += h[(size_t)i * bg::kCntSlots + k];
+    }
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z.data(), n * 8));
     return BGX_OK;
 }
 #endif

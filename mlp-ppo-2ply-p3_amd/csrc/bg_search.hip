@@ -48,8 +48,9 @@ namespace {
 // Work counters of the 2-ply enumerators (experiments, -DBGX_COUNTERS; tools/enum_counters.py):
 // this file's own set, apart from bg_core.h's move-generator counters
 #ifdef BGX_COUNTERS
-__device__ unsigned long long g_scnt[16];
-#define SC_CNT(i, v) do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_scnt[i], (unsigned long long)(v)); } while (0)
+__device__ unsigned long long g_scnt[16 * bg::kCntSlots];     // spread by workgroup (bg_core.h)
+#define SC_CNT(i, v) do { if ((threadIdx.x & 63) == 0) \
+    atomicAdd(&g_scnt[(i) * bg::kCntSlots + (blockIdx.x & (bg::kCntSlots - 1))], (unsigned long long)(v)); } while (0)
 #define SC_T0(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define SC_T1(i, t) SC_CNT(i, __builtin_amdgcn_s_memtime() - t)
 #else
@@ -1932,11 +1933,20 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
 // this translation unit's work counters (experiments; bg_engine.hip has its own set)
 int bgx_debug_search_counters(unsigned long long* out32) {
     SCK(hipDeviceSynchronize());
-    SCK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_scnt), 16 * 8));
-    SCK(hipMemcpyFromSymbol(out32 + 16, HIP_SYMBOL(bg::g_cnt), 16 * 8));   // the move generator's (bg_core.h)
-    unsigned long long z[16] = {0};
-    SCK(hipMemcpyToSymbol(HIP_SYMBOL(g_scnt), z, 16 * 8));
-    SCK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z, 16 * 8));
+    constexpr size_t n = 16 * (size_t)bg::kCntSlots;
+    std::vector<unsigned long long> h(n), z(n, 0ull);
+    SCK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_scnt), n * 8));
+    for (int i = 0; i < 16; ++i) {
+        out32[i] = 0;
+        for (int k = 0; k < bg::kCntSlots; ++k) out32[i] += h[(size_t)i * bg::kCntSlots + k];
+    }
+    SCK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(bg::g_cnt), n * 8));   // the move generator's (bg_core.h)
+    for (int i = 0; i < 16; ++i) {
+        out32[16 + i] = 0;
+        for (int k = 0; k < bg::kCntSlots; ++k) out32[16 + i] += h[(size_t)i * bg::kCntSlots + k];
+    }
+    SCK(hipMemcpyToSymbol(HIP_SYMBOL(g_scnt), z.data(), n * 8));
+    SCK(hipMemcpyToSymbol(HIP_SYMBOL(bg::g_cnt), z.data(), n * 8));
     return BGX_OK;
 }
 #endif
