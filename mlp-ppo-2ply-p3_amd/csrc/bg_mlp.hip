@@ -662,7 +662,36 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
         __builtin_amdgcn_wave_barrier();                // srec reads done before the next tile's stores
         float ss = 0.0f;                                // this lane's part of the row's |h|^2
-        if (row0 + j < n) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        if (hidden % 8 == 0) {
+            // the two lane halves of a row hold units 8q + 0..3 (h = 0) and 8q + 4..7 (h = 1):
+            // one v_permlane32_swap per dword pairs them, so that lane h writes the 16
+            // contiguous bytes of units 8(2p + h) + 0..7 (half the store instructions and
+            // request fragments of 8-byte stores)
+            _Float16* orow = hout + (size_t)(row0 + j) * hidden;
+            #pragma unroll
+            for (int t = 0; t < T; ++t)
+                #pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    h4 v[2];
+                    #pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int q = 2 * p + e, u = 32 * t + 8 * q + 4 * h;
+                        #pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            v[e][i] = (_Float16)fmaxf(acc[t][4 * q + i] + sb[u + i], 0.0f);
+                            if (u < hidden) ss = fmaf((float)v[e][i], (float)v[e][i], ss);
+                        }
+                    }
+                    const uint2 a = __builtin_bit_cast(uint2, v[0]), b = __builtin_bit_cast(uint2, v[1]);
+                    const auto s0 = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+                    const auto s1 = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+                    // lane h = 0: (units 8q0 + 0..3, 8q0 + 4..7); h = 1: (8q1 + 0..3, 8q1 + 4..7)
+                    const int u8 = 32 * t + 8 * (2 * p + h);
+                    if (row0 + j < n && u8 < hidden)
+                        *(uint4*)(orow + u8) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+                }
+        } else if (row0 + j < n) {
             _Float16* orow = hout + (size_t)(row0 + j) * hidden;
             #pragma unroll
             for (int t = 0; t < T; ++t)
@@ -670,7 +699,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                 for (int q = 0; q < 4; ++q) {           // units 32t + 8q + 4h + 0..3: one 8-byte store
                     const int u = 32 * t + 8 * q + 4 * h;
                     if (u < hidden) {
-                        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
                         h4 v;
                         #pragma unroll
                         for (int i = 0; i < 4; ++i) {
@@ -681,6 +709,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
                     }
                 }
         }
+        if (row0 + j >= n) ss = 0.0f;
         hm = fmaxf(hm, ss + __shfl_xor(ss, 32));        // this lane's row: both halves' parts
     }
     if (hmax2) {                                        // max |h_row|^2 of the workgroup, one atomic
