@@ -411,15 +411,25 @@ void k_ppo_rows(RowsArgs a, const int32_t* __restrict__ range) {
                     __asm__ volatile("" ::: "memory");
                 }
             }
-            if (valid) {
-                _Float16* dhr = a.dh + (size_t)row * kH + 32 * u + 4 * hh;
+            {
+                // units 32u + 8q + 4hh + 0..3 on lane half hh: one v_permlane32_swap per dword
+                // pairs the halves, so that lane hh stores the 16 contiguous bytes of units
+                // 32u + 8(2p + hh) + 0..7 (half the store instructions of 8-byte stores)
+                _Float16* dhr = a.dh + (size_t)row * kH + 32 * u;
                 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    f16x4 o;
+                for (int p = 0; p < 2; ++p) {
+                    f16x4 o[2];
                     #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        o[e] = (hm[u] >> (8 * q + 4 * hh + e)) & 1u ? (_Float16)dacc[4 * q + e] : (_Float16)0.0f;
-                    *(f16x4*)(dhr + 8 * q) = o;
+                    for (int c = 0; c < 2; ++c) {
+                        const int q = 2 * p + c;
+                        #pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            o[c][e] = (hm[u] >> (8 * q + 4 * hh + e)) & 1u ? (_Float16)dacc[4 * q + e] : (_Float16)0.0f;
+                    }
+                    const uint2 x = __builtin_bit_cast(uint2, o[0]), y = __builtin_bit_cast(uint2, o[1]);
+                    const auto s0 = __builtin_amdgcn_permlane32_swap(x.x, y.x, false, false);
+                    const auto s1 = __builtin_amdgcn_permlane32_swap(x.y, y.y, false, false);
+                    if (valid) *(uint4*)(dhr + 8 * (2 * p + hh)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
                 }
             }
         }
