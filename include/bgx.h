@@ -374,6 +374,15 @@ int bgx_ppo_gw1(const void* dh_dev, const uint8_t* records_dev, int32_t m, int32
 int bgx_lane_returns(const float* rewards_dev, const uint8_t* dones_dev, int32_t T, int32_t B, float gamma,
                      float* out_dev, void* stream);
 
+/* The episode accounting of a [T][B] rollout (the reference driver's per-env loop,
+ * train.py:55-99; bgx.train.episode_stats): records_dev uint8[T][B][64] (the mover is
+ * byte 52), carry_dev fp64[B] = each lane's reward of its unfinished episode, updated in
+ * place; out_dev fp64[6] = finished episodes, their summed rewards, wins, PLAYER1 wins,
+ * gammon wins, backgammon wins.  workspace of bgx_episode_stats_workspace(B) bytes. */
+int64_t bgx_episode_stats_workspace(int32_t B);
+int bgx_episode_stats(const float* rewards_dev, const uint8_t* dones_dev, const uint8_t* records_dev,
+                      double* carry_dev, int32_t T, int32_t B, double* workspace_dev, double* out_dev, void* stream);
+
 /* The PPO update's rollout rows in a given order, once per update (the fused head's
  * row plan, bgx.train.ppo_row_plan; the reference batches memory rows in order,
  * ppo_agent.py:235-266): row i of each output = row perm[i] of its input, for the

@@ -867,6 +867,59 @@ __global__ __launch_bounds__(256) void k_lane_returns(const float* __restrict__ 
     }
 }
 
+// ---- the rollout's episode accounting per game lane (bgx_episode_stats;
+// bgx.train.episode_stats restated, train.py:55-99): one thread per lane walks its T
+// steps, accumulating the unfinished episode's reward from the carry, closing it at each
+// done; per-block sums of the six statistics (fp64: the rewards are multiples of 1/2, so
+// every sum is exact in any order), then one block adds the block sums in order.  The
+// mover byte (record byte 52) is read only at winning steps.
+constexpr int kEpStats = 6;
+__global__ __launch_bounds__(256) void k_episode_partials(const float* __restrict__ r, const uint8_t* __restrict__ d,
+                                                          const uint8_t* __restrict__ rec, double* __restrict__ carry,
+                                                          int T, int B, double* __restrict__ part) {
+    __shared__ double red[4][kEpStats];
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    double v[kEpStats] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (b < B) {
+        double acc = carry[b];
+        for (int t = 0; t < T; ++t) {
+            const size_t i = (size_t)t * B + b;
+            const double rw = (double)r[i];
+            acc += rw;
+            if (d[i]) {
+                v[0] += 1.0;                               // finished episodes
+                v[1] += acc;                               // their rewards (carry included)
+                acc = 0.0;
+                if (rw > 0.0) {
+                    v[2] += 1.0;                           // wins (the mover of a winning step)
+                    v[3] += rec[i * 64 + 52] == 0 ? 1.0 : 0.0;     // by PLAYER1
+                }
+                v[4] += rw == 1.5 ? 1.0 : 0.0;             // gammon wins
+                v[5] += rw == 2.0 ? 1.0 : 0.0;             // backgammon wins
+            }
+        }
+        carry[b] = acc;
+    }
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    #pragma unroll
+    for (int k = 0; k < kEpStats; ++k) {
+        double x = v[k];
+        #pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+        if (l == 0) red[w][k] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < kEpStats)
+        part[(size_t)blockIdx.x * kEpStats + threadIdx.x] =
+            red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ __launch_bounds__(64) void k_episode_sum(const double* __restrict__ part, int nb, double* __restrict__ out) {
+    if (threadIdx.x >= kEpStats) return;
+    double s = 0.0;
+    for (int k = 0; k < nb; ++k) s += part[(size_t)k * kEpStats + threadIdx.x];
+    out[threadIdx.x] = s;
+}
+
 // ---- the update's rollout rows in plan order (bgx_gather_rollout): 4 threads per row,
 // each copying 16 bytes of the record; thread 0..3 of a row also copies one of the four
 // per-row fields
@@ -1153,6 +1206,9 @@ extern "C" int bgx_ppo_rows(const void* h, const int32_t* perm, const uint8_t* r
         const int need = (ntiles + waves - 1) / waves, g = grid > 0 ? grid : dflt;
         return dim3(need < g ? need : g);
     };
+    // (the 16-tile variant on a side stream beside the small ones, launched first, was
+    // measured slower: k_ppo_rows<1> 255 -> 392 us with a quarter of its LDS slots,
+    // update 7.27 -> 7.6 ms; profiles/r5/rejected/rows_fork)
     hipLaunchKernelGGL(k_ppo_rows<1>, wgs(4, 1024), dim3(256), 0, s, a, row_plan + 0);
     hipLaunchKernelGGL(k_ppo_rows<2>, wgs(4, 1024), dim3(256), 0, s, a, row_plan + 2);
     hipLaunchKernelGGL(k_ppo_rows<4>, wgs(4, 1024), dim3(256), 0, s, a, row_plan + 4);
@@ -1251,6 +1307,26 @@ extern "C" int bgx_ppo_plan(const uint8_t* records, int32_t m, int32_t n_actions
     if (nb > 0) hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, bcnt);
     hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, bcnt, nb, m, boff, plan, row_plan);
     if (nb > 0) hipLaunchKernelGGL(k_plan_scatter, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, boff, perm);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
+extern "C" int64_t bgx_episode_stats_workspace(int32_t B) {
+    if (B < 0) return BGX_EINVAL;
+    return (int64_t)((B + 255) / 256) * kEpStats * (int64_t)sizeof(double);
+}
+
+extern "C" int bgx_episode_stats(const float* rewards, const uint8_t* dones, const uint8_t* records, double* carry,
+                                 int32_t T, int32_t B, double* workspace, double* out, void* stream) {
+    if (T < 0 || B < 0 || !out || (B > 0 && (!carry || !workspace)) ||
+        (T > 0 && B > 0 && (!rewards || !dones || !records)))
+        return BGX_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const int nb = (B + 255) / 256;
+    if (nb > 0)
+        hipLaunchKernelGGL(k_episode_partials, dim3(nb), dim3(256), 0, s, rewards, dones, records, carry, T, B,
+                           workspace);
+    hipLaunchKernelGGL(k_episode_sum, dim3(1), dim3(64), 0, s, workspace, nb, out);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }

@@ -400,3 +400,22 @@ def test_update_graphs_match_eager(growth_interval):
         assert float(trs[0].scaler._scale.item()) == float(trs[1].scaler._scale.item())
         # loss parts: fp64 sums of per-workgroup partials in atomic order
         assert all(ms[0][k] == pytest.approx(ms[1][k], rel=1e-12, abs=1e-12) for k in ms[0]), it
+
+
+@pytest.mark.gpu
+def test_episode_stats_kernel_matches_torch():
+    """bgx_episode_stats (one HIP kernel per rollout) == bgx.train.episode_stats (the torch
+    form, itself checked against the reference driver's loop on the CPU): the six sums and
+    the updated per-lane carry, over two consecutive rollouts of a real trainer."""
+    from bgx.train import PPOTrainer, episode_stats, episode_stats_records
+    tr = PPOTrainer(batch=2048, horizon=24, seed=13, chunk=8192)
+    c1 = torch.zeros(2048, dtype=torch.float64, device="cuda")
+    c2 = c1.clone()
+    for _ in range(2):
+        tr.rollout()
+        b = tr.buf
+        a = episode_stats_records(b["rewards"], b["dones"], b["records"], c1)
+        r = episode_stats(b["rewards"], b["dones"], b["records"][:, :, 52], c2)
+        assert torch.equal(a, r), (a, r)
+        assert torch.equal(c1, c2)
+    assert float(a[0]) > 0
