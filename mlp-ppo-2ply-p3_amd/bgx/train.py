@@ -803,8 +803,11 @@ class PPOTrainer:
         torch.cuda.synchronize(self.dev)
         self._graphs = graphs
 
-    def rollout(self):
-        """T env steps on all B lanes (train.py:46-99 without the Python loops)."""
+    def rollout(self, defer_stats: bool = False):
+        """T env steps on all B lanes (train.py:46-99 without the Python loops).  Returns
+        the episodes finished; with defer_stats the episode statistics stay on the device
+        until the next update() reads them with its own final sync (iteration(): no host
+        sync, and so no idle GPU, between the rollout and the update) and None is returned."""
         self.net.pack(inplace=True)
         buf = self.buf
         cur = self._streams[0]
@@ -838,11 +841,19 @@ class PPOTrainer:
                     self._join_copies(k)
         for st in self._streams[1:]:
             cur.wait_stream(st)
+        if cur is not None and cur != torch.cuda.current_stream(self.dev):
+            torch.cuda.current_stream(self.dev).wait_stream(cur)   # the statistics and update() run there
         if self.graphs and self._graphs is None:
             self._capture()
         st = episode_stats_records(buf["rewards"], buf["dones"], buf["records"], self.ep_carry)
         if _world(self.group) > 1:
             dist.all_reduce(st, group=self.group)
+        if defer_stats:
+            self._pending_stats = st
+            return None
+        return self._apply_stats(st)
+
+    def _apply_stats(self, st):
         self.last_episode_stats = dict(zip(EPISODE_STATS, st.tolist()))
         eps = int(self.last_episode_stats["episodes"])
         self.total_episodes += eps
@@ -911,6 +922,9 @@ class PPOTrainer:
                 self._restore(snap)
                 self.fused_head = False
                 parts = self._epochs(recs, acts, old, R, adv, False)
+        if getattr(self, "_pending_stats", None) is not None:    # a deferred rollout's statistics
+            self._pending_eps = self._apply_stats(self._pending_stats)
+            self._pending_stats = None
         self.entropy_coef = entropy_coef_after_update(self.entropy_anneal, self.total_episodes)
         self._updates_done += 1
         p = (parts / NUM_EPOCHS).tolist()
@@ -1070,13 +1084,21 @@ class PPOTrainer:
                 off[t.dtype] += n
 
     def iteration(self):
+        # rollout and update back to back on the device (the episode statistics are read at
+        # the update's final sync); their split is timed with events
+        cur = torch.cuda.current_stream(self.dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         t0 = time.perf_counter()
-        eps = self.rollout()
-        torch.cuda.synchronize(self.dev)
-        t1 = time.perf_counter()
+        ev[0].record(cur)
+        self.rollout(defer_stats=True)
+        ev[1].record(cur)
         m = self.update()
+        ev[2].record(cur)
         torch.cuda.synchronize(self.dev)
         t2 = time.perf_counter()
+        eps = self._pending_eps
+        t_roll = ev[0].elapsed_time(ev[1]) * 1e-3
+        t1 = t0 + t_roll
         ws = _world(self.group)
         e = self.last_episode_stats
         k = max(e["episodes"], 1.0)
