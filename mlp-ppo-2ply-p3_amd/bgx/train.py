@@ -484,21 +484,36 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
     F_in = W1.shape[1]
     dev = W1.device
     k1 = float(np.float32(row_scale) * np.float32(c_e))      # the kernel's fp32 gscale * c_entropy
+    params = (W1, b1, Wa, ba, wv, bv)
+    # one launch for the casts, the packed fc1 fragments and the zeroed accumulators (and
+    # one for the gradient hand-off below) instead of ~20 small torch kernels per epoch
+    fast = F_in == 198 and all(t.dtype == torch.float32 and t.is_contiguous() for t in params)
     with torch.no_grad():
-        W1h, b1h = W1.half(), b1.half()
-        W2h = torch.zeros(512, Hd, dtype=torch.float16, device=dev)
-        b2h = torch.zeros(512, dtype=torch.float16, device=dev)
-        W2h[:A] = Wa.half(); W2h[A] = wv[0].half()
-        b2h[:A] = ba.half(); b2h[A] = bv[0].half()
-        gW1 = torch.zeros(Hd, 208, dtype=torch.float32, device=dev)
-        gW2 = torch.zeros(512, Hd, dtype=torch.float32, device=dev)
-        gb2 = torch.zeros(512, dtype=torch.float32, device=dev)
         L = _lib.load()
         p = lambda t: ctypes.c_void_p(t.data_ptr())
         stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         w1pack = torch.empty(L.bgx_fc1_packed_size(Hd), dtype=torch.uint8, device=dev)
-        check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
-        hmax2 = torch.zeros(1, dtype=torch.float32, device=dev) if guard is not None else None
+        if fast:
+            b1h = torch.empty(Hd, dtype=torch.float16, device=dev)
+            W2h = torch.empty(512, Hd, dtype=torch.float16, device=dev)
+            b2h = torch.empty(512, dtype=torch.float16, device=dev)
+            gW1 = torch.empty(Hd, 208, dtype=torch.float32, device=dev)
+            gW2 = torch.empty(512, Hd, dtype=torch.float32, device=dev)
+            gb2 = torch.empty(512, dtype=torch.float32, device=dev)
+            hmax2 = torch.empty(1, dtype=torch.float32, device=dev) if guard is not None else None
+            check(L.bgx_ppo_epoch_prep(*[p(t) for t in params], Hd, A, p(w1pack), p(b1h), p(W2h), p(b2h), p(gW1),
+                                       p(gW2), p(gb2), _ptr_or_none(hmax2), stream), "bgx_ppo_epoch_prep")
+        else:
+            W1h, b1h = W1.half(), b1.half()
+            W2h = torch.zeros(512, Hd, dtype=torch.float16, device=dev)
+            b2h = torch.zeros(512, dtype=torch.float16, device=dev)
+            W2h[:A] = Wa.half(); W2h[A] = wv[0].half()
+            b2h[:A] = ba.half(); b2h[A] = bv[0].half()
+            gW1 = torch.zeros(Hd, 208, dtype=torch.float32, device=dev)
+            gW2 = torch.zeros(512, Hd, dtype=torch.float32, device=dev)
+            gb2 = torch.zeros(512, dtype=torch.float32, device=dev)
+            check(L.bgx_fc1_pack(p(W1h), Hd, p(w1pack), stream), "bgx_fc1_pack")
+            hmax2 = torch.zeros(1, dtype=torch.float32, device=dev) if guard is not None else None
         for _feats, _legal, actions, old_logp, returns, adv, records, *extra in chunks:
             prep = extra[0] if extra else {}
             rec = records.contiguous()
@@ -523,6 +538,13 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
             # dh is in the order of rec (bgx_ppo_rows writes it in the original row order)
             ws1 = torch.empty(L.bgx_ppo_gw1_workspace(m) // 4, dtype=torch.float32, device=dev)
             check(L.bgx_ppo_gw1(p(dh), p(rec), m, Hd, p(ws1), p(gW1), stream), "bgx_ppo_gw1")
+        if fast:
+            grads = [torch.empty_like(t) for t in params]
+            check(L.bgx_ppo_epoch_grads(p(gW1), p(gW2), p(gb2), Hd, A, float(post), *[p(g) for g in grads], p(W2h),
+                                        p(b2h), _ptr_or_none(hmax2), float(MASK_SHORTCUT_LIMIT), _ptr_or_none(guard),
+                                        stream), "bgx_ppo_epoch_grads")
+            W1.grad, b1.grad, Wa.grad, ba.grad, wv.grad, bv.grad = grads
+            return
         if post != 1.0:
             for t in (gW1, gW2, gb2):
                 t.mul_(post)

@@ -725,6 +725,56 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void k
     }
 }
 
+// The fused fp16 PPO epoch's operands from the fp32 weights, and its zeroed gradient
+// accumulators, in one launch (bgx_ppo_epoch_prep; replaces a dozen torch casts, fills
+// and slice copies per epoch): the packed W1 fragments of fp16(W1) (k_fc1_pack's layout),
+// fp16(b1), W2h = fp16([action_head; value_head; 0]) [512][H], b2h, and zeros in gW1
+// [H][208], gW2 [512][H], gb2 [512] and hmax2.  fp16 conversions round to nearest, as
+// Tensor.half() does.
+struct EpochPrep {
+    const float *w1, *b1, *wa, *ba, *wv, *bv;
+    int hidden, n_actions, T;
+    uint4* w1pack;
+    _Float16 *b1h, *w2h, *b2h;
+    float *gw1, *gw2, *gb2, *hmax2;
+};
+__global__ __launch_bounds__(256) void k_ppo_epoch_prep(EpochPrep a) {
+    const int H = a.hidden, A = a.n_actions;
+    const long long n0 = (long long)kKB1 * a.T * 64, n1 = n0 + H, n2 = n1 + 512LL * H, n3 = n2 + 512,
+                    n4 = n3 + (long long)H * 208, n5 = n4 + 512LL * H, n6 = n5 + 512, n7 = n6 + 1;
+    for (long long g = (long long)blockIdx.x * 256 + threadIdx.x; g < n7; g += (long long)gridDim.x * 256) {
+        if (g < n0) {
+            const int l = (int)(g & 63), t = (int)((g >> 6) % a.T), kb = (int)((g >> 6) / a.T);
+            const int u = 32 * t + (l & 31);
+            f16x8 v;
+            #pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int src = kperm_src(kb, l >> 5, i);
+                v[i] = (u < H && src >= 0) ? (_Float16)a.w1[(size_t)u * kIn + src] : (_Float16)0.0f;
+            }
+            a.w1pack[g] = __builtin_bit_cast(uint4, v);
+        } else if (g < n1) {
+            const int u = (int)(g - n0);
+            a.b1h[u] = (_Float16)a.b1[u];
+        } else if (g < n2) {
+            const long long e = g - n1;
+            const int r = (int)(e / H), c = (int)(e % H);
+            a.w2h[e] = r < A ? (_Float16)a.wa[(size_t)r * H + c] : (r == A ? (_Float16)a.wv[c] : (_Float16)0.0f);
+        } else if (g < n3) {
+            const int r = (int)(g - n2);
+            a.b2h[r] = r < A ? (_Float16)a.ba[r] : (r == A ? (_Float16)a.bv[0] : (_Float16)0.0f);
+        } else if (g < n4) {
+            a.gw1[g - n3] = 0.0f;
+        } else if (g < n5) {
+            a.gw2[g - n4] = 0.0f;
+        } else if (g < n6) {
+            a.gb2[g - n5] = 0.0f;
+        } else if (a.hmax2) {
+            a.hmax2[0] = 0.0f;
+        }
+    }
+}
+
 __global__ void k_counter_add(uint32_t* ctr, uint32_t v) {
     if (threadIdx.x == 0) *ctr += v;
 }
@@ -835,6 +885,21 @@ int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* st
     const int T = (hidden + 31) / 32, work = kKB1 * T * 64;
     hipLaunchKernelGGL(k_fc1_pack, dim3((work + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                        (const _Float16*)w1h_dev, hidden, T, (uint4*)packed_dev);
+    return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
+}
+
+int bgx_ppo_epoch_prep(const float* w1_dev, const float* b1_dev, const float* wa_dev, const float* ba_dev,
+                       const float* wv_dev, const float* bv_dev, int32_t hidden, int32_t n_actions, void* w1pack_dev,
+                       void* b1h_dev, void* w2h_dev, void* b2h_dev, float* gw1_dev, float* gw2_dev, float* gb2_dev,
+                       float* hmax2_dev_or_null, void* stream) {
+    if (bgx_fc1_packed_size(hidden) < 0 || n_actions <= 0 || n_actions >= 512) return BGX_EINVAL;
+    if (!w1_dev || !b1_dev || !wa_dev || !ba_dev || !wv_dev || !bv_dev || !w1pack_dev || !b1h_dev || !w2h_dev ||
+        !b2h_dev || !gw1_dev || !gw2_dev || !gb2_dev || (uintptr_t)w1pack_dev % 16)
+        return BGX_EINVAL;
+    EpochPrep a{w1_dev, b1_dev, wa_dev, ba_dev, wv_dev, bv_dev, hidden, n_actions, (hidden + 31) / 32,
+                (uint4*)w1pack_dev, (_Float16*)b1h_dev, (_Float16*)w2h_dev, (_Float16*)b2h_dev, gw1_dev, gw2_dev,
+                gb2_dev, hmax2_dev_or_null};
+    hipLaunchKernelGGL(k_ppo_epoch_prep, dim3(512), dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }
 

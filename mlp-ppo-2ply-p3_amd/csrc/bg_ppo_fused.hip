@@ -1311,6 +1311,89 @@ extern "C" int bgx_ppo_plan(const uint8_t* records, int32_t m, int32_t n_actions
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }
 
+// The fused epoch's gradients into the parameters' .grad tensors, scaled by `post` in
+// fp32 (as Tensor.mul_ of the accumulators), in one launch (bgx_ppo_epoch_grads; replaces
+// three multiplies and six slice copies per epoch); block 0 also evaluates the masked-
+// action shortcut's bound: guard |= 2 (max_a |W2h[a]| sqrt(hmax2) + max_a |b2h[a]|) > limit
+// over the action rows a < A (the same quantities as the torch form, fp32).
+struct EpochGrads {
+    const float *gw1, *gw2, *gb2;
+    int hidden, n_actions;
+    float post;
+    float *w1g, *b1g, *wag, *bag, *wvg, *bvg;
+    const _Float16 *w2h, *b2h;
+    const float* hmax2;
+    float limit;
+    uint8_t* guard;
+};
+__global__ __launch_bounds__(256) void k_ppo_epoch_grads(EpochGrads a) {
+    const int H = a.hidden, A = a.n_actions;
+    if (blockIdx.x == 0 && a.guard) {
+        __shared__ float mn[256], mb[256];
+        float n2 = 0.0f, b = 0.0f;
+        for (int r = threadIdx.x; r < A; r += 256) {
+            float s = 0.0f;
+            for (int c = 0; c < H; ++c) {
+                const float w = (float)a.w2h[(size_t)r * H + c];
+                s = fmaf(w, w, s);
+            }
+            n2 = fmaxf(n2, sqrtf(s));
+            b = fmaxf(b, fabsf((float)a.b2h[r]));
+        }
+        mn[threadIdx.x] = n2;
+        mb[threadIdx.x] = b;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if (threadIdx.x < o) {
+                mn[threadIdx.x] = fmaxf(mn[threadIdx.x], mn[threadIdx.x + o]);
+                mb[threadIdx.x] = fmaxf(mb[threadIdx.x], mb[threadIdx.x + o]);
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            const float U = mn[0] * sqrtf(a.hmax2[0]) + mb[0];
+            if (2.0f * U > a.limit) a.guard[0] = 1;
+        }
+        return;
+    }
+    const long long n0 = (long long)H * 198, n1 = n0 + H, n2 = n1 + (long long)A * H, n3 = n2 + A, n4 = n3 + H,
+                    n5 = n4 + 1;
+    const int nb = a.guard ? gridDim.x - 1 : gridDim.x, b0 = a.guard ? blockIdx.x - 1 : blockIdx.x;
+    for (long long g = (long long)b0 * 256 + threadIdx.x; g < n5; g += (long long)nb * 256) {
+        if (g < n0) {
+            const int u = (int)(g / 198), f = (int)(g % 198);
+            a.w1g[g] = a.gw1[(size_t)u * 208 + f] * a.post;
+        } else if (g < n1) {
+            const int u = (int)(g - n0);
+            a.b1g[u] = a.gw1[(size_t)u * 208 + 198] * a.post;
+        } else if (g < n2) {
+            a.wag[g - n1] = a.gw2[g - n1] * a.post;
+        } else if (g < n3) {
+            a.bag[g - n2] = a.gb2[g - n2] * a.post;
+        } else if (g < n4) {
+            a.wvg[g - n3] = a.gw2[(size_t)A * H + (g - n3)] * a.post;
+        } else {
+            a.bvg[0] = a.gb2[A] * a.post;
+        }
+    }
+}
+
+extern "C" int bgx_ppo_epoch_grads(const float* gw1_dev, const float* gw2_dev, const float* gb2_dev, int32_t hidden,
+                                   int32_t n_actions, float post, float* w1_grad, float* b1_grad, float* wa_grad,
+                                   float* ba_grad, float* wv_grad, float* bv_grad, const void* w2h_dev,
+                                   const void* b2h_dev, const float* hmax2_dev, float limit, uint8_t* guard_dev_or_null,
+                                   void* stream) {
+    if (hidden <= 0 || hidden > 128 || n_actions <= 0 || n_actions >= 512) return BGX_EINVAL;
+    if (!gw1_dev || !gw2_dev || !gb2_dev || !w1_grad || !b1_grad || !wa_grad || !ba_grad || !wv_grad || !bv_grad)
+        return BGX_EINVAL;
+    if (guard_dev_or_null && (!w2h_dev || !b2h_dev || !hmax2_dev)) return BGX_EINVAL;
+    EpochGrads a{gw1_dev, gw2_dev, gb2_dev, hidden, n_actions, post, w1_grad, b1_grad, wa_grad, ba_grad, wv_grad,
+                 bv_grad, (const _Float16*)w2h_dev, (const _Float16*)b2h_dev, hmax2_dev, limit, guard_dev_or_null};
+    hipLaunchKernelGGL(k_ppo_epoch_grads, dim3(guard_dev_or_null ? 257 : 256), dim3(256), 0, (hipStream_t)stream, a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+}
+
 extern "C" int64_t bgx_episode_stats_workspace(int32_t B) {
     if (B < 0) return BGX_EINVAL;
     return (int64_t)((B + 255) / 256) * kEpStats * (int64_t)sizeof(double);
