@@ -501,8 +501,10 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
             gW2 = torch.empty(512, Hd, dtype=torch.float32, device=dev)
             gb2 = torch.empty(512, dtype=torch.float32, device=dev)
             hmax2 = torch.empty(1, dtype=torch.float32, device=dev) if guard is not None else None
+            bound = torch.empty(2, 512, dtype=torch.float32, device=dev) if guard is not None else None
             check(L.bgx_ppo_epoch_prep(*[p(t) for t in params], Hd, A, p(w1pack), p(b1h), p(W2h), p(b2h), p(gW1),
-                                       p(gW2), p(gb2), _ptr_or_none(hmax2), stream), "bgx_ppo_epoch_prep")
+                                       p(gW2), p(gb2), _ptr_or_none(hmax2), _ptr_or_none(bound), stream),
+                  "bgx_ppo_epoch_prep")
         else:
             W1h, b1h = W1.half(), b1.half()
             W2h = torch.zeros(512, Hd, dtype=torch.float16, device=dev)
@@ -540,9 +542,9 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
             check(L.bgx_ppo_gw1(p(dh), p(rec), m, Hd, p(ws1), p(gW1), stream), "bgx_ppo_gw1")
         if fast:
             grads = [torch.empty_like(t) for t in params]
-            check(L.bgx_ppo_epoch_grads(p(gW1), p(gW2), p(gb2), Hd, A, float(post), *[p(g) for g in grads], p(W2h),
-                                        p(b2h), _ptr_or_none(hmax2), float(MASK_SHORTCUT_LIMIT), _ptr_or_none(guard),
-                                        stream), "bgx_ppo_epoch_grads")
+            check(L.bgx_ppo_epoch_grads(p(gW1), p(gW2), p(gb2), Hd, A, float(post), *[p(g) for g in grads],
+                                        _ptr_or_none(bound), _ptr_or_none(hmax2), float(MASK_SHORTCUT_LIMIT),
+                                        _ptr_or_none(guard), stream), "bgx_ppo_epoch_grads")
             W1.grad, b1.grad, Wa.grad, ba.grad, wv.grad, bv.grad = grads
             return
         if post != 1.0:

@@ -737,9 +737,26 @@ struct EpochPrep {
     uint4* w1pack;
     _Float16 *b1h, *w2h, *b2h;
     float *gw1, *gw2, *gb2, *hmax2;
+    float* bound;        // [2][512]: |fp16(action row a)| and |fp16(action bias a)| (may be NULL)
 };
 __global__ __launch_bounds__(256) void k_ppo_epoch_prep(EpochPrep a) {
     const int H = a.hidden, A = a.n_actions;
+    if (a.bound) {                          // one wave per action row, lanes over its columns
+        const int r = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
+        if (r < A) {
+            float s = 0.0f;
+            for (int c = l; c < H; c += 64) {
+                const float v = (float)(_Float16)a.wa[(size_t)r * H + c];
+                s = fmaf(v, v, s);
+            }
+            #pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+            if (l == 0) {
+                a.bound[r] = sqrtf(s);
+                a.bound[512 + r] = fabsf((float)(_Float16)a.ba[r]);
+            }
+        }
+    }
     const long long n0 = (long long)kKB1 * a.T * 64, n1 = n0 + H, n2 = n1 + 512LL * H, n3 = n2 + 512,
                     n4 = n3 + (long long)H * 208, n5 = n4 + 512LL * H, n6 = n5 + 512, n7 = n6 + 1;
     for (long long g = (long long)blockIdx.x * 256 + threadIdx.x; g < n7; g += (long long)gridDim.x * 256) {
@@ -891,14 +908,14 @@ int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* st
 int bgx_ppo_epoch_prep(const float* w1_dev, const float* b1_dev, const float* wa_dev, const float* ba_dev,
                        const float* wv_dev, const float* bv_dev, int32_t hidden, int32_t n_actions, void* w1pack_dev,
                        void* b1h_dev, void* w2h_dev, void* b2h_dev, float* gw1_dev, float* gw2_dev, float* gb2_dev,
-                       float* hmax2_dev_or_null, void* stream) {
+                       float* hmax2_dev_or_null, float* bound_dev_or_null, void* stream) {
     if (bgx_fc1_packed_size(hidden) < 0 || n_actions <= 0 || n_actions >= 512) return BGX_EINVAL;
     if (!w1_dev || !b1_dev || !wa_dev || !ba_dev || !wv_dev || !bv_dev || !w1pack_dev || !b1h_dev || !w2h_dev ||
         !b2h_dev || !gw1_dev || !gw2_dev || !gb2_dev || (uintptr_t)w1pack_dev % 16)
         return BGX_EINVAL;
     EpochPrep a{w1_dev, b1_dev, wa_dev, ba_dev, wv_dev, bv_dev, hidden, n_actions, (hidden + 31) / 32,
                 (uint4*)w1pack_dev, (_Float16*)b1h_dev, (_Float16*)w2h_dev, (_Float16*)b2h_dev, gw1_dev, gw2_dev,
-                gb2_dev, hmax2_dev_or_null};
+                gb2_dev, hmax2_dev_or_null, bound_dev_or_null};
     hipLaunchKernelGGL(k_ppo_epoch_prep, dim3(512), dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }

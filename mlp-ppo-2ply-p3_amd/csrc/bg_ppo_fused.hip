@@ -1315,30 +1315,26 @@ extern "C" int bgx_ppo_plan(const uint8_t* records, int32_t m, int32_t n_actions
 // fp32 (as Tensor.mul_ of the accumulators), in one launch (bgx_ppo_epoch_grads; replaces
 // three multiplies and six slice copies per epoch); block 0 also evaluates the masked-
 // action shortcut's bound: guard |= 2 (max_a |W2h[a]| sqrt(hmax2) + max_a |b2h[a]|) > limit
-// over the action rows a < A (the same quantities as the torch form, fp32).
+// over the action rows a < A (the same quantities as the torch form, fp32; the per-row
+// norms come from bgx_ppo_epoch_prep, one wave per row).
 struct EpochGrads {
     const float *gw1, *gw2, *gb2;
     int hidden, n_actions;
     float post;
     float *w1g, *b1g, *wag, *bag, *wvg, *bvg;
-    const _Float16 *w2h, *b2h;
     const float* hmax2;
     float limit;
     uint8_t* guard;
+    const float* bound;         // [2][512] from bgx_ppo_epoch_prep
 };
 __global__ __launch_bounds__(256) void k_ppo_epoch_grads(EpochGrads a) {
     const int H = a.hidden, A = a.n_actions;
     if (blockIdx.x == 0 && a.guard) {
         __shared__ float mn[256], mb[256];
         float n2 = 0.0f, b = 0.0f;
-        for (int r = threadIdx.x; r < A; r += 256) {
-            float s = 0.0f;
-            for (int c = 0; c < H; ++c) {
-                const float w = (float)a.w2h[(size_t)r * H + c];
-                s = fmaf(w, w, s);
-            }
-            n2 = fmaxf(n2, sqrtf(s));
-            b = fmaxf(b, fabsf((float)a.b2h[r]));
+        for (int r = threadIdx.x; r < A; r += 256) {       // the row bounds bgx_ppo_epoch_prep wrote
+            n2 = fmaxf(n2, a.bound[r]);
+            b = fmaxf(b, a.bound[512 + r]);
         }
         mn[threadIdx.x] = n2;
         mb[threadIdx.x] = b;
@@ -1380,15 +1376,14 @@ __global__ __launch_bounds__(256) void k_ppo_epoch_grads(EpochGrads a) {
 
 extern "C" int bgx_ppo_epoch_grads(const float* gw1_dev, const float* gw2_dev, const float* gb2_dev, int32_t hidden,
                                    int32_t n_actions, float post, float* w1_grad, float* b1_grad, float* wa_grad,
-                                   float* ba_grad, float* wv_grad, float* bv_grad, const void* w2h_dev,
-                                   const void* b2h_dev, const float* hmax2_dev, float limit, uint8_t* guard_dev_or_null,
-                                   void* stream) {
+                                   float* ba_grad, float* wv_grad, float* bv_grad, const float* bound_dev,
+                                   const float* hmax2_dev, float limit, uint8_t* guard_dev_or_null, void* stream) {
     if (hidden <= 0 || hidden > 128 || n_actions <= 0 || n_actions >= 512) return BGX_EINVAL;
     if (!gw1_dev || !gw2_dev || !gb2_dev || !w1_grad || !b1_grad || !wa_grad || !ba_grad || !wv_grad || !bv_grad)
         return BGX_EINVAL;
-    if (guard_dev_or_null && (!w2h_dev || !b2h_dev || !hmax2_dev)) return BGX_EINVAL;
+    if (guard_dev_or_null && (!bound_dev || !hmax2_dev)) return BGX_EINVAL;
     EpochGrads a{gw1_dev, gw2_dev, gb2_dev, hidden, n_actions, post, w1_grad, b1_grad, wa_grad, ba_grad, wv_grad,
-                 bv_grad, (const _Float16*)w2h_dev, (const _Float16*)b2h_dev, hmax2_dev, limit, guard_dev_or_null};
+                 bv_grad, hmax2_dev, limit, guard_dev_or_null, bound_dev};
     hipLaunchKernelGGL(k_ppo_epoch_grads, dim3(guard_dev_or_null ? 257 : 256), dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
