@@ -50,7 +50,9 @@ enum bgx_status {
  * a HIP graph are ordered by the graph: its launch stream must follow whatever else
  * used the engine, and a call after a graph launch on another stream must be ordered
  * by the caller.  Kernels that take raw lane pointers (bgx_policy_act*, reading
- * bgx_buffers.lanes) run on the caller's stream as given.  bgx_two_ply returns
+ * bgx_buffers.lanes) run on the caller's stream as given.  The host-side state calls
+ * without a stream (bgx_engine_seed, bgx_engine_mt_state, bgx_engine_error) synchronise
+ * the device before and after.  bgx_two_ply returns
  * BGX_ESTATE (and bgx_one_ply sets bit 1 of the engine's error word) if it finds a
  * lane whose legal moves no longer match its row layout, instead of reading past them. */
 
@@ -334,7 +336,8 @@ int bgx_fc1_records_ex(const uint8_t* records_dev, int32_t n, const void* packed
  * dh [m][128] fp16 = ReLU'(h) * fp16(dy W2h) (original row order), and the row
  * statistics stats [m] (16 B, 16-byte aligned) + info [m] (int32) in perm order
  * for bgx_ppo_gw2; dy_or_null [m][512] fp16 receives dy = [dlogits | dvalue | 0]
- * (tests).  row_plan int32[8] = the row tiles (of perm order) [lo, hi) handled by
+ * and z_or_null [m][512] fp16 the logits [y | value] of the 32-column tiles the row's
+ * variant computed (other columns untouched) -- both for tests.  row_plan int32[8] = the row tiles (of perm order) [lo, hi) handled by
  * the variants for at most 1, 2, 4 and 16 leading action tiles (every row tile in
  * exactly one range; a tile's count is the largest of its rows').  grid <= 0:
  * persistent grids of 4 workgroups per CU (1 for the 16-tile variant).
@@ -349,7 +352,8 @@ int bgx_ppo_rows(const void* h_dev, const int32_t* perm_dev, const uint8_t* reco
                  const float* old_logp_dev, const float* returns_dev, const float* adv_dev, int32_t m, int32_t hidden,
                  int32_t n_actions, const void* w2h_dev, const void* b2h_dev, float eps_clip, float c_value,
                  float c_entropy, float grad_scale, void* dh_dev, void* stats_dev, int32_t* info_dev,
-                 double* sums_dev, void* dy_or_null, const int32_t* row_plan_dev, int32_t grid, void* stream);
+                 double* sums_dev, void* dy_or_null, void* z_or_null, const int32_t* row_plan_dev, int32_t grid,
+                 void* stream);
 int64_t bgx_ppo_gw2_workspace(int32_t m);
 int bgx_ppo_gw2(const void* h_dev, const int32_t* perm_dev, const void* stats_dev, const int32_t* info_dev, int32_t m,
                 int32_t hidden, int32_t n_actions, const void* w2h_dev, const void* b2h_dev, float k1,
@@ -442,6 +446,18 @@ int bgx_gather_rollout(const int32_t* perm_dev, int32_t n, const uint8_t* record
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf
  * evaluation after it (k_eval, the MFMA kernel). */
 int bgx_two_ply_timings(bgx_engine* e, float* ms2);
+
+/* Debug options (tests and diagnostics only; the product path never reads the
+ * environment).  Sets option `name` to `value` (NULL: unset) for the process.  Names:
+ * BGX_2PLY_HEAVY "log:memo" (9:0 / 10:0: the doubles enumerator without the memo / with
+ * a 1,024-slot table), BGX_2PLY_LDS_CAP "first[:mid]" (forced overflow tiers),
+ * BGX_2PLY_POOL n (leaf-pool slots: retry rounds), BGX_2PLY_UNFACTORED (the 13-k-block
+ * evaluator), BGX_2PLY_BARROW 0 (bar rows per job), BGX_2PLY_DUMP path (pool, row sides,
+ * V per slot), BGX_2PLY_DEBUG (round sizes on stderr), BGX_POLICY_SKIP 0 (no tile skip),
+ * BGX_POLICY_HEAVY n (the policy's heavy-row bound); read at engine creation: BGX_XCD 0,
+ * BGX_ORDER 0 (lane-order dispatch), BGX_STAMPS, BGX_STEP_DEBUG.  Every alternative is
+ * exact: results are identical, only the schedule or the diagnostics change. */
+int bgx_debug_option(const char* name, const char* value_or_null);
 
 /* Last HIP error string of this thread (diagnostics). */
 const char* bgx_last_error(void);

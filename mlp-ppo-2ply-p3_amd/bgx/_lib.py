@@ -66,7 +66,7 @@ SIGNATURES = {
     "bgx_fc1_records": (ctypes.c_int, [_P, _I32, _P, _P, _I32, _P, _P]),
     "bgx_fc1_records_ex": (ctypes.c_int, [_P, _I32, _P, _P, _I32, _P, _P, _P]),
     "bgx_ppo_rows": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P, _P, ctypes.c_float,
-                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _I32, _P]),
+                                    ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _I32, _P]),
     "bgx_ppo_gw2_workspace": (ctypes.c_int64, [_I32]),
     "bgx_ppo_gw2": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P]),
     "bgx_ppo_gw1_workspace": (ctypes.c_int64, [_I32]),
@@ -85,6 +85,7 @@ SIGNATURES = {
     "bgx_gather_rollout": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "bgx_ppo_plan_workspace": (ctypes.c_int64, [_I32]),
     "bgx_ppo_plan": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
+    "bgx_debug_option": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),
 }
@@ -152,7 +153,36 @@ def load():
     return _lib
 
 
+STATUS_NAMES = {BGX_EINVAL: "BGX_EINVAL", BGX_EDEVICE: "BGX_EDEVICE", BGX_ENOMEM: "BGX_ENOMEM",
+                BGX_EOVERFLOW: "BGX_EOVERFLOW", BGX_ESTATE: "BGX_ESTATE"}
+
+
 def check(rc: int, what: str):
     if rc != BGX_OK:
         msg = load().bgx_last_error()
-        raise BgxError(f"{what} failed: status {rc} ({msg.decode() if msg else ''})")
+        raise BgxError(f"{what} failed: status {rc} {STATUS_NAMES.get(rc, '')} ({msg.decode() if msg else ''})")
+
+
+def debug_option(name: str, value=None):
+    """bgx_debug_option: set (value str/int) or unset (None) one of the library's named
+    debug options (include/bgx.h: the exact alternative paths the tests compare, and
+    diagnostics).  The library never reads the environment."""
+    check(load().bgx_debug_option(name.encode(), None if value is None else str(value).encode()),
+          f"bgx_debug_option({name})")
+
+
+class debug_options:
+    """Context manager: set debug options for a block, unset them after."""
+
+    def __init__(self, **opts):
+        self.opts = opts
+
+    def __enter__(self):
+        for k, v in self.opts.items():
+            debug_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.opts:
+            debug_option(k, None)
+        return False

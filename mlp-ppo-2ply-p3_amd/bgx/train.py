@@ -531,7 +531,7 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
             old, ret, ad = old_logp.float().contiguous(), returns.float().contiguous(), adv.float().contiguous()
             pp = None if perm is None else p(perm)             # None: rows already in plan order
             check(L.bgx_ppo_rows(p(h), pp, p(rec), p(acts), p(old), p(ret), p(ad), m, Hd, A, p(W2h), p(b2h),
-                                 eps, c_v, c_e, row_scale, p(dh), p(stats), p(info), p(sums), None, p(row_plan), 0,
+                                 eps, c_v, c_e, row_scale, p(dh), p(stats), p(info), p(sums), None, None, p(row_plan), 0,
                                  stream),
                   "bgx_ppo_rows")
             ws = torch.empty(L.bgx_ppo_gw2_workspace(m) // 4, dtype=torch.float32, device=dev)
@@ -712,6 +712,7 @@ class PPOTrainer:
                                and not (dist.is_available() and dist.is_initialized()))
                               if update_graphs is None else bool(update_graphs))
         self._ugraph = None            # (key, graph, loss-parts output)
+        self._ugraph_captures = 0
         self._ubufs = None             # persistent per-chunk rows in plan order + plans
         self._updates_done = 0
         # fork (Engine.set_fork): an env step's light launch on the engine's side stream.
@@ -873,6 +874,8 @@ class PPOTrainer:
         if _world(self.group) > 1:
             dist.all_reduce(st, group=self.group)
         if defer_stats:
+            if getattr(self, "_pending_stats", None) is not None:   # an earlier deferred rollout, no update since
+                self._apply_stats(self._pending_stats)
             self._pending_stats = st
             return None
         return self._apply_stats(st)
@@ -1042,8 +1045,9 @@ class PPOTrainer:
         parts = None
         cur = torch.cuda.current_stream(self.dev)
         for _ in range(NUM_EPOCHS):
-            key = (hint["scale"], float(self.entropy_coef), N)
+            key = self._ugraph_key(hint["scale"], N)
             if self._ugraph is None or self._ugraph[0] != key:
+                self._ugraph_captures += 1
                 self._ugraph = None
                 st = torch.cuda.Stream(self.dev)
                 st.wait_stream(cur)
@@ -1107,6 +1111,25 @@ class PPOTrainer:
                 t.copy_(flat[t.dtype][off[t.dtype]:off[t.dtype] + n].view_as(t))
                 off[t.dtype] += n
 
+    def _ugraph_key(self, scale, N):
+        """What the captured update graph bakes in: the GradScaler scale, the entropy
+        coefficient and the row count (kernel arguments), Adam's lr / betas / eps (passed by
+        value to bgx_adam_step), and the device addresses of every parameter, its Adam state
+        and the scaler's tensors (an optimizer or scaler reload replaces them).  Any change
+        recaptures."""
+        grp = self.opt.param_groups[0]
+        ptrs = []
+        for p in self.net.parameters():
+            ptrs.append(p.data_ptr())
+            st = self.opt.state.get(p, {})
+            ptrs.extend(st[k].data_ptr() if torch.is_tensor(st.get(k)) else None
+                        for k in ("exp_avg", "exp_avg_sq", "step"))
+        for k in ("_scale", "_growth_tracker"):
+            t = getattr(self.scaler, k, None)
+            ptrs.append(t.data_ptr() if torch.is_tensor(t) else None)
+        return (scale, float(self.entropy_coef), N, float(grp["lr"]), tuple(float(b) for b in grp["betas"]),
+                float(grp["eps"]), id(self.opt), id(self.scaler), tuple(ptrs))
+
     def iteration(self):
         # rollout and update back to back on the device (the episode statistics are read at
         # the update's final sync); their split is timed with events
@@ -1121,15 +1144,16 @@ class PPOTrainer:
         torch.cuda.synchronize(self.dev)
         t2 = time.perf_counter()
         eps = self._pending_eps
+        # both phases on the GPU's clock (ev 0 -> 1 -> 2); the wall time covers the host too
         t_roll = ev[0].elapsed_time(ev[1]) * 1e-3
-        t1 = t0 + t_roll
+        t_upd = ev[1].elapsed_time(ev[2]) * 1e-3
         ws = _world(self.group)
         e = self.last_episode_stats
         k = max(e["episodes"], 1.0)
         m.update({"avg_episode_reward": e["episode_reward_sum"] / k, "win_rate": e["wins"] / k,
                   "p1_win_rate": e["p1_wins"] / k, "gammon_rate": e["gammons"] / k,
                   "backgammon_rate": e["backgammons"] / k, "total_episodes": self.total_episodes})
-        m.update({"episodes": eps, "env_steps": self.B * self.T * ws, "rollout_s": t1 - t0, "update_s": t2 - t1,
+        m.update({"episodes": eps, "env_steps": self.B * self.T * ws, "rollout_s": t_roll, "update_s": t_upd,
                   "env_steps_per_s": self.B * self.T * ws / (t2 - t0), "entropy_coef": self.entropy_coef})
         return m
 

@@ -416,6 +416,7 @@ __device__ __forceinline__ void store_rec(const Args& A, int gi, int bv) { A.lan
 
 // Engine object behind the C ABI's opaque bgx_engine*.
 struct bgx_engine {
+    bool step_debug = false;        // BGX_STEP_DEBUG (bgx_debug_option) at creation: per-step tier sizes
     int device;
     bg::Args a;
     uint4* slow_tables;

@@ -21,6 +21,8 @@
 #include <vector>
 
 #include "bg_engine.h"
+#include "bg_debug.h"
+#include <map>
 
 using namespace bg;
 
@@ -497,8 +499,21 @@ int fail(hipError_t e, int code = BGX_EDEVICE) {
 }  // namespace
 
 
-// error hook for the other translation units (bg_search.hip)
+// error hooks for the other translation units (bg_search.hip, bg_ppo*.hip)
 int bgx_internal_fail(hipError_t e) { return fail(e); }
+void bgx_set_error(const char* msg) { g_err = msg; }
+// the explicit debug options (bg_debug.h, bgx_debug_option)
+static std::mutex g_dbg_mu;
+static std::map<std::string, std::string> g_dbg;
+std::string bgx_dbg(const char* name) {
+    std::lock_guard<std::mutex> g(g_dbg_mu);
+    const auto it = g_dbg.find(name);
+    return it == g_dbg.end() ? std::string() : it->second;
+}
+long long bgx_dbg_int(const char* name, long long dflt) {
+    const std::string v = bgx_dbg(name);
+    return v.empty() ? dflt : strtoll(v.c_str(), nullptr, 10);
+}
 
 #define CK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return fail(_e); } while (0)
 // the per-position kernels (reset, standalone movegen, regeneration) with the
@@ -574,8 +589,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     A.B = batch; A.max_moves = max_moves; A.dice_mode = dice_mode; A.auto_reset = auto_reset ? 1 : 0;
     A.match_length = match_length;
     A.key0 = (uint32_t)seed; A.key1 = (uint32_t)(seed >> 32);
-    const char* xc = getenv("BGX_XCD");
-    A.xcd = batch % 128 == 0 && !(xc && xc[0] == '0') ? 1 : 0;
+    A.xcd = batch % 128 == 0 && bgx_dbg_int("BGX_XCD", 1) != 0 ? 1 : 0;
+    e->step_debug = !bgx_dbg("BGX_STEP_DEBUG").empty();
     e->slow_waves = kSlowWaves;
     const size_t B = (size_t)batch;
     hipError_t err = hipSuccess;
@@ -591,9 +606,8 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     alloc((void**)&A.ovf_queue, 2 * B * 4);
     alloc((void**)&A.err, 16);
     alloc((void**)&e->slow_tables, (size_t)kSlowWaves * ((size_t)16 << kLogSlotsSlow));
-    if (getenv("BGX_STAMPS")) alloc((void**)&A.stamps, B * 16);
-    const char* so = getenv("BGX_ORDER");
-    if (dice_mode == BGX_DICE_PHILOX && !(so && so[0] == '0')) {
+    if (!bgx_dbg("BGX_STAMPS").empty()) alloc((void**)&A.stamps, B * 16);
+    if (dice_mode == BGX_DICE_PHILOX && bgx_dbg_int("BGX_ORDER", 1) != 0) {
         alloc((void**)&e->perm, B * 4);
         alloc((void**)&A.cls, B);
         alloc((void**)&e->order_cnt, (B / 1024 + 1) * kXcd * kClasses * 4);
@@ -660,9 +674,15 @@ int bgx_engine_seed(bgx_engine* e, const uint32_t* seeds_host, uint64_t philox_s
     if (!e || !seeds_host) return BGX_EINVAL;
     CK(hipSetDevice(e->device));
     Args& A = e->a;
+    // device-wide order (bgx.h "Stream ordering"): every earlier call on any stream has
+    // finished before the dice state changes, and the new state is in place on return
+    CK(hipDeviceSynchronize());
     A.key0 = (uint32_t)philox_seed; A.key1 = (uint32_t)(philox_seed >> 32);
     CK(hipMemset(A.ctr, 0, (size_t)A.B * 8));
-    if (A.dice_mode == BGX_DICE_PHILOX) return BGX_OK;
+    if (A.dice_mode == BGX_DICE_PHILOX) {
+        CK(hipDeviceSynchronize());
+        return BGX_OK;
+    }
     const int n = A.dice_mode == BGX_DICE_MT_LANE ? A.B : 1;
     uint32_t* dseeds = nullptr;
     CK(hipMalloc(&dseeds, (size_t)n * 4));
@@ -826,7 +846,7 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
     }
     CKL();
     const int rc = slow_path(e, s, 0, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
-    if (getenv("BGX_STEP_DEBUG")) {          // overflow-tier queue sizes of this step
+    if (e->step_debug) {                     // overflow-tier queue sizes of this step
         int32_t q[2] = {0, 0};
         CK(hipMemcpyAsync(q, A.ovf_count, 8, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
@@ -1012,6 +1032,13 @@ int bgx_copy_regions(const bgx_region* regions, int32_t n, int32_t workgroups, v
 }
 
 const char* bgx_last_error(void) { return g_err.c_str(); }
+
+int bgx_debug_option(const char* name, const char* value) {
+    if (!name || !name[0]) return BGX_EINVAL;
+    std::lock_guard<std::mutex> g(g_dbg_mu);
+    if (value) g_dbg[name] = value; else g_dbg.erase(name);
+    return BGX_OK;
+}
 
 #ifndef BGX_BUILD_ID
 #define BGX_BUILD_ID "unknown"

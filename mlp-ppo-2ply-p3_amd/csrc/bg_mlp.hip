@@ -24,6 +24,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include "../../include/bgx.h"
+#include "bg_debug.h"
 
 
 namespace {
@@ -843,12 +844,11 @@ int bgx_policy_act_ctr(const uint8_t* records_dev, int32_t n, const float* packe
     const uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
     const bool plain = !greedy && !logits_out;
     // the masked-action tile skip (k_policy_act, MODE 0): 2 extra waves per kZWin rows for count-0 rows
-    const char* sv = getenv("BGX_POLICY_SKIP");     // read per call: tests compare both paths in one process
-    const bool skip = !(sv && sv[0] == '0');
+    // (tests compare both paths in one process through bgx_debug_option)
+    const bool skip = bgx_dbg_int("BGX_POLICY_SKIP", 1) != 0;
     // rows with more legal actions than this go to the extra workgroups too (their tiles split
     // four ways), so no main wave walks more than ceil(heavy / 32) action tiles (round 5)
-    const char* hv = getenv("BGX_POLICY_HEAVY");
-    const int heavy = hv ? atoi(hv) : kHeavyDefault;
+    const int heavy = (int)bgx_dbg_int("BGX_POLICY_HEAVY", kHeavyDefault);
     const dim3 grid0(skip ? n_wg + 2 * ((n + kZWin - 1) / kZWin) : n_wg);
 #define BGX_ACT(TT)                                                                                           \
     do {                                                                                                      \

@@ -136,6 +136,7 @@ struct RowsArgs {
     int32_t* info;              // [m] sorted order: act | lim << 16
     double* sums;               // policy loss, value error^2, entropy sums
     _Float16* dy;               // optional [m][512] dL/dy (tests), original row order
+    _Float16* z;                // optional [m][512] fp16 logits of the tiles computed (tests), original row order
 };
 
 // One variant per bound TM on the leading action tiles a row tile needs (TM = 1, 2, 4,
@@ -268,6 +269,8 @@ void k_ppo_rows(RowsArgs a, const int32_t* __restrict__ range) {
                         const int i = 4 * q + e;
                         const _Float16 zh = (_Float16)(acc[i] + bq[e]);
                         if (k == kVk && i == kVi) v_own = (float)zh;
+                        if (a.z && valid)
+                            a.z[(size_t)row * kAp + 32 * BGX_TILE_T(k) + (i & 3) + 8 * (i >> 2) + 4 * hh] = zh;
                         if (kKeep) {
                             const int ko = (i & 3) + 8 * (i >> 2);
                             TZ[kKeep ? k : 0][i] = ko < lt ? (float)zh * kL2e : -INFINITY;
@@ -1187,17 +1190,18 @@ extern "C" int bgx_ppo_rows(const void* h, const int32_t* perm, const uint8_t* r
                             const float* old_logp, const float* returns, const float* adv, int32_t m, int32_t hidden,
                             int32_t n_actions, const void* w2h, const void* b2h, float eps_clip, float c_value,
                             float c_entropy, float grad_scale, void* dh, void* stats, int32_t* info, double* sums,
-                            void* dy, const int32_t* row_plan, int32_t grid, void* stream) {
+                            void* dy, void* z, const int32_t* row_plan, int32_t grid, void* stream) {
     if (hidden != kH || n_actions != kA || m < 0) return BGX_EINVAL;
     if (m == 0) return BGX_OK;
     if (!h || !records || !actions || !old_logp || !returns || !adv || !w2h || !b2h || !dh || !stats ||
         !info || !sums || !row_plan)
         return BGX_EINVAL;
-    if (((uintptr_t)h | (uintptr_t)w2h | (uintptr_t)stats | (uintptr_t)dy) % 16 || ((uintptr_t)dh | (uintptr_t)b2h) % 8)
+    if (((uintptr_t)h | (uintptr_t)w2h | (uintptr_t)stats | (uintptr_t)dy) % 16 || ((uintptr_t)dh | (uintptr_t)b2h) % 8 ||
+        (uintptr_t)z % 2)
         return BGX_EINVAL;
     RowsArgs a{(const _Float16*)h, perm, records, actions, old_logp, returns, adv, (const _Float16*)w2h,
                (const _Float16*)b2h, m, eps_clip, c_value, c_entropy, grad_scale, (_Float16*)dh, (float4*)stats,
-               info, sums, (_Float16*)dy};
+               info, sums, (_Float16*)dy, (_Float16*)z};
     hipStream_t s = (hipStream_t)stream;
     const int ntiles = (m + 31) / 32;
     // persistent grids: at most enough workgroups for every row tile, else `grid` (<= 0:

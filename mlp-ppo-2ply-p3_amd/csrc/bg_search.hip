@@ -40,6 +40,7 @@
 #include <string.h>
 
 #include "bg_engine.h"
+#include "bg_debug.h"
 
 using namespace bg;
 
@@ -1112,6 +1113,29 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
         float a[NN];
         #pragma unroll
         for (int n = 0; n < NN; ++n) a[n] = 0.0f;
+#if defined(BGX_EXP_OPSEL_ASM)
+        // EXPERIMENT (round 6): the SLP build's packed value head restated as inline asm
+        // in the no-SLP build: tile 0 low, tile 1 high, odd weights by op_sel:[0,1,0]
+        static_assert(NN == 2, "two tiles");
+        typedef float f32x2e __attribute__((ext_vector_type(2)));
+        f32x2e acc = {0.0f, 0.0f};
+        #pragma unroll
+        for (int t = 0; t < NA; ++t)
+            #pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const float4 w = reinterpret_cast<const float4*>(wvs)[(t * 4 + r4) * 64 + l + z];
+                const f32x2e wxy = {w.x, w.y}, wzw = {w.z, w.w};
+                f32x2e p[4];
+                #pragma unroll
+                for (int j = 0; j < 4; ++j) p[j] = (f32x2e){relu_raw(x[0][t][4 * r4 + j]), relu_raw(x[1][t][4 * r4 + j])};
+                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]\n\ts_nop 0" : "+v"(acc) : "v"(p[0]), "v"(wxy));
+                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0]\n\ts_nop 0" : "+v"(acc) : "v"(p[1]), "v"(wxy));
+                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]\n\ts_nop 0" : "+v"(acc) : "v"(p[2]), "v"(wzw));
+                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0]\n\ts_nop 0" : "+v"(acc) : "v"(p[3]), "v"(wzw));
+            }
+        a[0] = acc.x;
+        a[1] = acc.y;
+#else
         #pragma unroll
         for (int t = 0; t < NA; ++t)
             #pragma unroll
@@ -1123,8 +1147,13 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
                     a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 1]), w.y, a[n]);
                     a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 2]), w.z, a[n]);
                     a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 3]), w.w, a[n]);
+#if defined(BGX_EXP_NOPACK)
+                    // EXPERIMENT (round 6): opaque per tile, so SLP cannot pack the two tiles
+                    __asm__ volatile("" : "+v"(a[n]));
+#endif
                 }
             }
+#endif
         #pragma unroll
         for (int n = 0; n < NN; ++n) v[n] = a[n] + __shfl_xor(a[n], 32) + bias;
     } else {
@@ -1550,6 +1579,7 @@ __global__ __launch_bounds__(256) void k_expand(Args A, const int32_t* lane_off,
 }  // namespace
 
 extern int bgx_internal_fail(hipError_t e);
+extern void bgx_set_error(const char* msg);
 #define SCK(x) do { hipError_t _e = (x); if (_e != hipSuccess) return bgx_internal_fail(_e); } while (0)
 
 static int value_tiles16(int H) { return (H + 15) / 16; }   // 16 hidden units (hi + lo rows) per MFMA tile
@@ -1748,19 +1778,19 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         hipLaunchKernelGGL(k_rows, dim3((rows + 3) / 4 < 16384 ? (rows + 3) / 4 : 16384), dim3(256), 0, s, A, row_lane,
                            lane_off, &ctr->rows, rowrec, rowside, nullptr, &ctr->bad);
         SCK(hipGetLastError());
-        const char* brw = getenv("BGX_2PLY_BARROW");      // tests: the bar rows per job instead
+        const bool barrow = bgx_dbg_int("BGX_2PLY_BARROW", 1) != 0;      // tests: 0 = the bar rows per job
         S2 S{rowrec, 0, rows, nullptr, nullptr, &ctr->cursor, 0ull, maxlen, &ctr->leaves,
              ctr->qcount, (int32_t*)(ws + o_q), &ctr->retry_count,
              retry, list, &ctr->list_count, A.err, cap_fast<kLogLight>(), 0, cap_fast<kLogMid>(), 3, 3,
-             brw && brw[0] == '0' ? 0 : 1};
+             barrow ? 1 : 0};
         // doubles enumerator: 512-slot dedup table with the revisit memo inside it, held to
         // 128 VGPRs (4 waves/SIMD, +1.5 %).  Tests (BGX_2PLY_HEAVY = 9:0 / 10:0) run the
         // exact alternatives without the memo (9:0) or with a 1,024-slot table (10:0): the
         // same leaves, Q and choices (tests/test_gpu_search.py)
         int hlog = 9, hmk = 2;
-        if (const char* hv = getenv("BGX_2PLY_HEAVY")) {
-            hlog = atoi(hv);
-            const char* c = strchr(hv, ':');
+        if (const std::string hv = bgx_dbg("BGX_2PLY_HEAVY"); !hv.empty()) {
+            hlog = atoi(hv.c_str());
+            const char* c = strchr(hv.c_str(), ':');
             hmk = c ? atoi(c + 1) : 2;
         }
         void (*kheavy)(S2) = k_enum<9, 2, 1, 4>;
@@ -1769,16 +1799,16 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         else if (hlog == 10 && hmk == 0) { kheavy = k_enum<10, 0, 1>; klist = k_enum<10, 0, 2>; }
         else { hlog = 9; hmk = 2; }
         S.cap_heavy = (7 << hlog) / 8;
-        if (const char* fs = getenv("BGX_2PLY_LDS_CAP")) {    // tests: force the overflow tiers ("first[:mid]")
-            S.cap_light = S.cap_heavy = S.cap_mid = atoi(fs);
-            if (const char* c = strchr(fs, ':')) S.cap_mid = atoi(c + 1);
+        if (const std::string fs = bgx_dbg("BGX_2PLY_LDS_CAP"); !fs.empty()) {    // tests: force the overflow tiers ("first[:mid]")
+            S.cap_light = S.cap_heavy = S.cap_mid = atoi(fs.c_str());
+            if (const char* c = strchr(fs.c_str(), ':')) S.cap_mid = atoi(c + 1);
         }
-        const bool dbg = getenv("BGX_2PLY_DEBUG") != nullptr;
+        const bool dbg = !bgx_dbg("BGX_2PLY_DEBUG").empty();
         const float* f16s = vpacked;
         const uint4* w1q = (const uint4*)(f16s + 4);
         // the root mover's part of X1 per row (the factored evaluator); BGX_2PLY_UNFACTORED
         // (tests) evaluates every leaf over all 13 k-blocks instead
-        const bool factored = getenv("BGX_2PLY_UNFACTORED") == nullptr;
+        const bool factored = bgx_dbg("BGX_2PLY_UNFACTORED").empty();
         if (factored)
             hipLaunchKernelGGL(rowpart_kernel(NT), dim3((rows + 127) / 128 < 8192 ? (rows + 127) / 128 : 8192), dim3(256),
                                0, s, rowside, &ctr->rows, w1q, rowpart);
@@ -1796,7 +1826,7 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         // BGX_2PLY_POOL overrides (tests force retry rounds with a tiny pool)
         // every resident wave may hold a partly filled block in each tier
         size_t cap = (size_t)jobs * 32 + (size_t)(g_light + g_heavy + g_list + g_t0 + g_mid + e->slow_waves) * kBlk * 2;
-        if (const char* ps = getenv("BGX_2PLY_POOL")) cap = (size_t)strtoull(ps, nullptr, 10);
+        if (const long long ps = bgx_dbg_int("BGX_2PLY_POOL", 0); ps > 0) cap = (size_t)ps;
         cap = (cap + kBlk - 1) / kBlk * kBlk;
         if (cap < (size_t)kBlk * 4) cap = (size_t)kBlk * 4;
         if (cap > ((size_t)1 << 31)) cap = (size_t)1 << 31;
@@ -1814,7 +1844,8 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
         E.tags = S.tags;
         S.cap = E.cap = (unsigned long long)pcap;
         float* vdbg = nullptr;
-        if (getenv("BGX_2PLY_DUMP")) {
+        const std::string dump = bgx_dbg("BGX_2PLY_DUMP");
+        if (!dump.empty()) {
             SCK(hipMalloc(&vdbg, pcap * 4));
             SCK(hipMemsetAsync(vdbg, 0, pcap * 4, s));
             E.vdbg = vdbg;
@@ -1865,7 +1896,10 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
             SCK(hipMemcpyAsync(&hc, ctr, sizeof hc, hipMemcpyDeviceToHost, s));
             SCK(hipStreamSynchronize(s));
             const int32_t nretry = hc.retry_count;
-            if (hc.bad) return BGX_ESTATE;     // the lanes changed under the call (bgx.h stream ordering)
+            if (hc.bad) {                      // the lanes changed under the call (bgx.h stream ordering)
+                bgx_set_error("bgx_two_ply: the lanes' move lists changed under the call (stream ordering)");
+                return BGX_ESTATE;
+            }
             if (round == 0) {
                 SCK(hipEventElapsedTime(&e->search_ms[0], e->search_ev[0], e->search_ev[1]));
                 SCK(hipEventElapsedTime(&e->search_ms[1], e->search_ev[1], e->search_ev[2]));
@@ -1875,7 +1909,8 @@ int bgx_two_ply(bgx_engine* e, const float* vpacked, int32_t hidden, float value
                         hc.cursor, pcap, hc.qcount[0] + hc.qcount[1], hc.qcount[2], hc.retry_count, hc.leaves);
             if (nretry == 0) {
                 // test hook (tests/test_gpu_search.py): per-job minv, row parts, the pool, V per slot
-                if (const char* dp = getenv("BGX_2PLY_DUMP")) {
+                if (!dump.empty()) {
+                    const char* dp = dump.c_str();
                     int32_t* hm = (int32_t*)malloc((size_t)jobs * 4);
                     SCK(hipMemcpy(hm, minv, (size_t)jobs * 4, hipMemcpyDeviceToHost));
                     FILE* f = fopen(dp, "wb");

@@ -23,3 +23,26 @@ def golden():
     def load(name):
         return dict(np.load(os.path.join(GOLDEN, name + ".npz")))
     return load
+
+
+@pytest.fixture
+def dbg():
+    """The library's explicit debug options (bgx_debug_option, include/bgx.h) with a
+    monkeypatch-like interface; every option set is unset at teardown."""
+    from bgx import _lib
+
+    class Dbg:
+        def __init__(self):
+            self.names = set()
+
+        def setenv(self, name, value):
+            _lib.debug_option(name, value)
+            self.names.add(name)
+
+        def delenv(self, name, raising=True):
+            _lib.debug_option(name, None)
+
+    d = Dbg()
+    yield d
+    for n in d.names:
+        _lib.debug_option(n, None)

@@ -257,7 +257,7 @@ def test_philox_split_dispatch_vs_oracle(bgx):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B", [16384, 1000])
-def test_dispatch_order_does_not_change_results(bgx, monkeypatch, B):
+def test_dispatch_order_does_not_change_results(bgx, dbg, B):
     """The dispatch order (class-sorted, XCD-aware 16-lane runs when B % 128 == 0,
     plain class sort otherwise, or no order at all with the run swizzle) only
     schedules: every variant must step every lane exactly once and give the same
@@ -266,9 +266,9 @@ def test_dispatch_order_does_not_change_results(bgx, monkeypatch, B):
     engs = []
     for env in variants:
         for k in ("BGX_XCD", "BGX_ORDER"):
-            monkeypatch.delenv(k, raising=False)
+            dbg.delenv(k, raising=False)
         for k, v in env.items():
-            monkeypatch.setenv(k, v)
+            dbg.setenv(k, v)
         e = bgx.Engine(batch=B, max_moves=500, dice="philox", seed=21, auto_reset=True)
         e.reset(want_obs=False)
         engs.append(e)

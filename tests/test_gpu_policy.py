@@ -176,12 +176,12 @@ def test_rollout_path_in_place(bgx):
     assert e1.error() == 0 and e2.error() == 0
 
 
-def _act_both(net, rec, seed, step, monkeypatch):
-    monkeypatch.setenv("BGX_POLICY_SKIP", "1")
+def _act_both(net, rec, seed, step, dbg):
+    dbg.setenv("BGX_POLICY_SKIP", "1")
     on = [t.clone() for t in net.act(rec, seed=seed, step=step)]
-    monkeypatch.setenv("BGX_POLICY_SKIP", "0")
+    dbg.setenv("BGX_POLICY_SKIP", "0")
     off = [t.clone() for t in net.act(rec, seed=seed, step=step)]
-    monkeypatch.delenv("BGX_POLICY_SKIP")
+    dbg.delenv("BGX_POLICY_SKIP")
     return on, off
 
 
@@ -198,7 +198,7 @@ def _assert_same(on, off, rec):
 
 
 @pytest.mark.parametrize("heavy", ["64", "32", "1000"])
-def test_policy_tile_skip_matches_full_pass(bgx, monkeypatch, heavy):
+def test_policy_tile_skip_matches_full_pass(bgx, dbg, heavy):
     """The masked-action tile skip and the extra waves (bg_mlp.hip, k_policy_act MODE 0:
     rows with no legal move or more than BGX_POLICY_HEAVY legal actions gathered into
     workgroups that split the action tiles four ways; 1000 = count-0 rows only, the
@@ -206,7 +206,7 @@ def test_policy_tile_skip_matches_full_pass(bgx, monkeypatch, heavy):
     (count-0 rows, doubles with hundreds of moves), a window with more gathered rows
     than the extra waves take, a ragged batch, and weights whose logit bound is too
     loose for any skip."""
-    monkeypatch.setenv("BGX_POLICY_HEAVY", heavy)
+    dbg.setenv("BGX_POLICY_HEAVY", heavy)
     from bgx.policy import PolicyNet
     torch.manual_seed(0)
     net = PolicyNet(hidden_size=128).cuda()
@@ -216,7 +216,7 @@ def test_policy_tile_skip_matches_full_pass(bgx, monkeypatch, heavy):
     for i in range(24):
         rec = eng.records()
         zero_rows += int((rec[:, 60].int() | rec[:, 61].int()).eq(0).sum())
-        on, off = _act_both(net, rec, 7, i, monkeypatch)
+        on, off = _act_both(net, rec, 7, i, dbg)
         _assert_same(on, off, rec)
         eng.step(on[0])
     assert zero_rows > 0
@@ -224,10 +224,10 @@ def test_policy_tile_skip_matches_full_pass(bgx, monkeypatch, heavy):
     rec[300:420, 60:62] = 0                              # 120 count-0 rows in one 256-row window
     rec[1000:1010, 60] = 244                             # 500 legal actions
     rec[1000:1010, 61] = 1
-    _assert_same(*_act_both(net, rec, 9, 0, monkeypatch), rec)
-    _assert_same(*_act_both(net, rec[:5000 - 17], 9, 1, monkeypatch), rec[:5000 - 17])
+    _assert_same(*_act_both(net, rec, 9, 0, dbg), rec)
+    _assert_same(*_act_both(net, rec[:5000 - 17], 9, 1, dbg), rec[:5000 - 17])
     big = PolicyNet(hidden_size=128).cuda()
     with torch.no_grad():
         big.load_state_dict(net.state_dict())
         big.action_head.weight.mul_(40.0)
-    _assert_same(*_act_both(big, rec, 9, 2, monkeypatch), rec)
+    _assert_same(*_act_both(big, rec, 9, 2, dbg), rec)

@@ -167,7 +167,7 @@ def test_two_ply_targeted_roots_vs_oracle(setup, targeted_roots):
     assert big >= 20, big                              # doubles reply sets over 100 moves
 
 
-def test_two_ply_factored_matches_full_form(setup, monkeypatch):
+def test_two_ply_factored_matches_full_form(setup, dbg):
     """The factored evaluator (the root mover's part of X1 once per row, then the
     replier's k-blocks, block 12 and the hit deltas per leaf) against the full
     13-k-block form on every leaf (BGX_2PLY_UNFACTORED): Q within 1e-5, the same
@@ -175,7 +175,7 @@ def test_two_ply_factored_matches_full_form(setup, monkeypatch):
     bgx, net, vh, eng = setup
     from bgx.search import two_ply
     best, bestq, q, st = two_ply(eng, vh, want_q=True)
-    monkeypatch.setenv("BGX_2PLY_UNFACTORED", "1")
+    dbg.setenv("BGX_2PLY_UNFACTORED", "1")
     best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
     assert st2 == st
     n = eng.n_moves()
@@ -187,13 +187,13 @@ def test_two_ply_factored_matches_full_form(setup, monkeypatch):
     assert torch.equal(best[clear], best2[clear])
 
 
-def test_two_ply_pool_retry_rounds(setup, monkeypatch):
+def test_two_ply_pool_retry_rounds(setup, dbg):
     """A leaf pool far too small for one pass: lost jobs are re-run in later
     rounds; Q, the choice and the exact leaf count must not change."""
     bgx, net, vh, eng = setup
     from bgx.search import two_ply
     best, bestq, q, st = two_ply(eng, vh, want_q=True)
-    monkeypatch.setenv("BGX_2PLY_POOL", "65536")
+    dbg.setenv("BGX_2PLY_POOL", "65536")
     best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
     assert st2["leaves"] == st["leaves"]
     assert torch.equal(torch.nan_to_num(q2, 7.0), torch.nan_to_num(q, 7.0))
@@ -202,7 +202,7 @@ def test_two_ply_pool_retry_rounds(setup, monkeypatch):
 
 @pytest.mark.parametrize("caps", ["6:3584", "6"])
 @pytest.mark.parametrize("heavy", ["9:2", "9:0", "10:0"])
-def test_two_ply_overflow_tiers(setup, monkeypatch, caps, heavy):
+def test_two_ply_overflow_tiers(setup, dbg, caps, heavy):
     """Every reply enumeration forced out of its first LDS table: into the
     4,096-slot LDS tier ("6:3584") or on through it to the HBM-table tier ("6").
     Same Q, choice and leaf count as the normal path."""
@@ -216,8 +216,8 @@ def test_two_ply_overflow_tiers(setup, monkeypatch, caps, heavy):
         nm = eng.n_moves().cpu().numpy()
         eng.step(torch.from_numpy(np.array([rng.randint(k) if k else 0 for k in nm], np.int32)).cuda())
     best, bestq, q, st = two_ply(eng, vh, want_q=True)
-    monkeypatch.setenv("BGX_2PLY_HEAVY", heavy)
-    monkeypatch.setenv("BGX_2PLY_LDS_CAP", caps)
+    dbg.setenv("BGX_2PLY_HEAVY", heavy)
+    dbg.setenv("BGX_2PLY_LDS_CAP", caps)
     best2, bestq2, q2, st2 = two_ply(eng, vh, want_q=True)
     assert eng.error() == 0
     assert st2["leaves"] == st["leaves"]
@@ -225,7 +225,7 @@ def test_two_ply_overflow_tiers(setup, monkeypatch, caps, heavy):
     assert torch.equal(best2, best)
 
 
-def test_two_ply_full_batch_paths_agree(monkeypatch):
+def test_two_ply_full_batch_paths_agree(dbg):
     """C4 at full size (B = 65,536 roots after 60 self-play steps): the doubles
     enumerator with its revisit memo inside a 512-slot table and with a
     1,024-slot table plus separate memo tables (different tier traffic, pruning
@@ -245,15 +245,15 @@ def test_two_ply_full_batch_paths_agree(monkeypatch):
         eng.step(a, want_obs=False, want_info=False)
     vh = ValueHead(PolicyNet(hidden_size=40).cuda())
     b1, q1, Q1, s1 = two_ply(eng, vh, want_q=True)
-    monkeypatch.setenv("BGX_2PLY_HEAVY", "10:0")
+    dbg.setenv("BGX_2PLY_HEAVY", "10:0")
     b2, q2, Q2, s2 = two_ply(eng, vh, want_q=True)
     assert s1 == s2
     assert torch.equal(torch.nan_to_num(Q1, 7.0), torch.nan_to_num(Q2, 7.0))
     assert torch.equal(b1, b2) and torch.equal(q1, q2)
     # the rows whose replier is on the bar: the table-free row walk (nd_row_bar) against
     # the per-job walks it replaces
-    monkeypatch.delenv("BGX_2PLY_HEAVY")
-    monkeypatch.setenv("BGX_2PLY_BARROW", "0")
+    dbg.delenv("BGX_2PLY_HEAVY")
+    dbg.setenv("BGX_2PLY_BARROW", "0")
     b3, q3, Q3, s3 = two_ply(eng, vh, want_q=True)
     assert s1 == s3
     assert torch.equal(torch.nan_to_num(Q1, 7.0), torch.nan_to_num(Q3, 7.0))
@@ -312,7 +312,7 @@ def _leaf_reference(net, keys, tags, side, ml):
 
 
 @pytest.mark.parametrize("unfactored", [False, True])
-def test_two_ply_every_leaf_vs_fp64(setup, monkeypatch, tmp_path, unfactored):
+def test_two_ply_every_leaf_vs_fp64(setup, dbg, tmp_path, unfactored):
     """Every surviving leaf of the 48-root batch (~534 k): the evaluator's V (the
     BGX_2PLY_DUMP test hook writes V per pool slot with the pool, row sides and max
     lengths) against an fp64 MLP on the leaf's own encoding, within 1e-6 -- the factored
@@ -322,9 +322,9 @@ def test_two_ply_every_leaf_vs_fp64(setup, monkeypatch, tmp_path, unfactored):
     bgx, net, vh, eng = setup
     from bgx.search import two_ply
     pre = str(tmp_path / "d")
-    monkeypatch.setenv("BGX_2PLY_DUMP", pre)
+    dbg.setenv("BGX_2PLY_DUMP", pre)
     if unfactored:
-        monkeypatch.setenv("BGX_2PLY_UNFACTORED", "1")
+        dbg.setenv("BGX_2PLY_UNFACTORED", "1")
     two_ply(eng, vh)
     keys = np.fromfile(pre + ".keys", np.uint32).reshape(-1, 4)
     tags = np.fromfile(pre + ".tags", np.uint32)

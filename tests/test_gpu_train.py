@@ -375,6 +375,53 @@ def test_update_redone_after_skipped_step(monkeypatch):
         assert torch.allclose(a, b, rtol=1e-6, atol=0)
 
 
+def test_graphed_update_redone_after_nonfinite(monkeypatch):
+    """The graphed update's non-finite-step path: one clean update, then a
+    rollout whose rewards hold an inf, so every epoch's gradient is non-finite.  The
+    graphed trainer replays its captured epochs with the scale baked in at capture (the
+    device skips each step and backs the scale off), finds the host hint stale after the
+    update, restores its snapshot and redoes the update eagerly; the result equals, bit
+    for bit, an eager trainer without the scale hint.  A third, clean update then runs
+    on a recaptured graph (the scale changed) and still matches."""
+    from bgx.train import PPOTrainer
+    g = PPOTrainer(batch=8192, horizon=4, seed=21, update_graphs=True)
+    e = PPOTrainer(batch=8192, horizon=4, seed=21, update_graphs=False)
+    monkeypatch.setattr(e, "_scale_state", lambda: None)
+    for it in range(3):
+        for tr in (g, e):
+            tr.rollout()
+            if it == 1:
+                tr.buf["rewards"][1, 7] = float("inf")
+            tr.update()
+        torch.cuda.synchronize()
+        for a, b in zip(g.net.parameters(), e.net.parameters()):
+            assert torch.equal(a, b), it
+            assert torch.equal(g.opt.state[a]["exp_avg"], e.opt.state[b]["exp_avg"]), it
+            assert torch.equal(g.opt.state[a]["exp_avg_sq"], e.opt.state[b]["exp_avg_sq"]), it
+        assert float(g.scaler._scale.item()) == float(e.scaler._scale.item()), it
+        assert all(torch.isfinite(p).all() for p in g.net.parameters())
+    assert float(g.scaler._scale.item()) < 65536.0       # the non-finite steps backed the scale off
+    assert g._ugraph is not None and g._ugraph_captures >= 1
+
+
+def test_update_graph_recaptured_on_optimizer_change():
+    """The captured update graph's key holds Adam's lr (passed by value to bgx_adam_step)
+    and the addresses of the optimizer's state: changing lr between updates recaptures
+    and the result equals an eager trainer with the same lr schedule."""
+    from bgx.train import PPOTrainer
+    trs = [PPOTrainer(batch=8192, horizon=4, seed=5, update_graphs=gr) for gr in (False, True)]
+    for it in range(4):
+        for tr in trs:
+            if it == 2:
+                tr.opt.param_groups[0]["lr"] = 3e-4
+            tr.rollout()
+            tr.update()
+        torch.cuda.synchronize()
+        for a, b in zip(trs[0].net.parameters(), trs[1].net.parameters()):
+            assert torch.equal(a, b), it
+    assert trs[1]._ugraph_captures == 2                  # at the second update, again after the lr change
+
+
 @pytest.mark.parametrize("growth_interval", [2000, 3])
 def test_update_graphs_match_eager(growth_interval):
     """The update's fused-head epoch replayed as a HIP graph (captured at the second

@@ -48,9 +48,10 @@ def main():
     for trial in range(int(os.environ.get("TRIALS", "3"))):
         d = tempfile.mkdtemp()
         prefix = os.path.join(d, "d")
-        os.environ["BGX_2PLY_DUMP"] = prefix
+        from bgx._lib import debug_option
+        debug_option("BGX_2PLY_DUMP", prefix)
         two_ply(eng, vh)
-        del os.environ["BGX_2PLY_DUMP"]
+        debug_option("BGX_2PLY_DUMP", None)
         keys = np.fromfile(prefix + ".keys", np.uint32).reshape(-1, 4)
         tags = np.fromfile(prefix + ".tags", np.uint32)
         v = np.fromfile(prefix + ".v", np.float32)

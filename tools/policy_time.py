@@ -24,7 +24,8 @@ cnt = (rec[:, 60].int() | (rec[:, 61].int() << 8))
 print(f"B={B} count0 {float((cnt == 0).float().mean()):.3f} >32 {float((cnt > 32).float().mean()):.3f} "
       f">128 {float((cnt > 128).float().mean()):.3f}")
 for sk in ("1", "0", "1", "0"):
-    os.environ["BGX_POLICY_SKIP"] = sk
+    from bgx._lib import debug_option
+    debug_option("BGX_POLICY_SKIP", sk)
     for _ in range(5):
         net.act(rec, seed=2, step=0)
     torch.cuda.synchronize()

@@ -1,9 +1,10 @@
 """Diagnostics: per-wave start/end of k_step (BGX_STAMPS=1) -> residency profile."""
 import ctypes, os, sys
-os.environ["BGX_STAMPS"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "mlp-ppo-2ply-p3_amd")]
 import numpy as np, torch, bgx
+from bgx._lib import debug_option
+debug_option("BGX_STAMPS", 1)            # read at engine creation
 from bgx.policy import PolicyNet
 B = 65536
 eng = bgx.Engine(batch=B, dice="philox", seed=5)
