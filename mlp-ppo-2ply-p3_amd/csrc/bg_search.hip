@@ -1113,29 +1113,6 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
         float a[NN];
         #pragma unroll
         for (int n = 0; n < NN; ++n) a[n] = 0.0f;
-#if defined(BGX_EXP_OPSEL_ASM)
-        // EXPERIMENT (round 6): the SLP build's packed value head restated as inline asm
-        // in the no-SLP build: tile 0 low, tile 1 high, odd weights by op_sel:[0,1,0]
-        static_assert(NN == 2, "two tiles");
-        typedef float f32x2e __attribute__((ext_vector_type(2)));
-        f32x2e acc = {0.0f, 0.0f};
-        #pragma unroll
-        for (int t = 0; t < NA; ++t)
-            #pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-                const float4 w = reinterpret_cast<const float4*>(wvs)[(t * 4 + r4) * 64 + l + z];
-                const f32x2e wxy = {w.x, w.y}, wzw = {w.z, w.w};
-                f32x2e p[4];
-                #pragma unroll
-                for (int j = 0; j < 4; ++j) p[j] = (f32x2e){relu_raw(x[0][t][4 * r4 + j]), relu_raw(x[1][t][4 * r4 + j])};
-                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]\n\ts_nop 0" : "+v"(acc) : "v"(p[0]), "v"(wxy));
-                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0]\n\ts_nop 0" : "+v"(acc) : "v"(p[1]), "v"(wxy));
-                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]\n\ts_nop 0" : "+v"(acc) : "v"(p[2]), "v"(wzw));
-                asm volatile("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0]\n\ts_nop 0" : "+v"(acc) : "v"(p[3]), "v"(wzw));
-            }
-        a[0] = acc.x;
-        a[1] = acc.y;
-#else
         #pragma unroll
         for (int t = 0; t < NA; ++t)
             #pragma unroll
@@ -1147,13 +1124,8 @@ __device__ __forceinline__ void eval_leaves_fact(const uint4* wq, const float* w
                     a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 1]), w.y, a[n]);
                     a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 2]), w.z, a[n]);
                     a[n] = fmaf(relu_raw(x[n][t][4 * r4 + 3]), w.w, a[n]);
-#if defined(BGX_EXP_NOPACK)
-                    // EXPERIMENT (round 6): opaque per tile, so SLP cannot pack the two tiles
-                    __asm__ volatile("" : "+v"(a[n]));
-#endif
                 }
             }
-#endif
         #pragma unroll
         for (int n = 0; n < NN; ++n) v[n] = a[n] + __shfl_xor(a[n], 32) + bias;
     } else {
