@@ -193,6 +193,10 @@ def cpu_baseline(seconds: float):
            "sample": f"{multi_steps} random-policy BackgammonEnv.step calls of the C oracle (oracle/bgoracle.c), "
                      f"{procs} processes x 1 thread, {seconds:.0f} s",
            "cores_available": avail, "host_cpus": os.cpu_count(),
+           "cores_note": ("16 processes: the GPU box's CPU share per GPU is 16 (its OMP_NUM_THREADS / MAX_JOBS "
+                          f"are {os.environ.get('OMP_NUM_THREADS', '?')}; the pool's rules size worker pools to that "
+                          "share); the affinity mask and cpu_count show the whole machine's CPUs, which the other "
+                          "GPUs' jobs share.  The port scales linearly per process (single_core x cores ~= value)"),
            "single_core": {"value": one, "steps": one_steps, "seconds": seconds}}
     ref = os.path.join(ROOT, "profiles", "cpu_reference_timing.json")
     if os.path.exists(ref):
@@ -664,7 +668,12 @@ def main():
     torch.cuda.synchronize(dev)
     barrier(ws)
     torch.cuda.synchronize(dev)
+    # the timed region on the device clock too: a HIP event on every shard's stream before
+    # its first and after its last timed step (the roofline's step window)
+    tev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(S)]
     t0 = time.perf_counter()
+    for k in range(S):
+        tev[k][0].record(streams[k])
     if graphs:
         for r in range(args.steps // G):
             row = graphs[r % len(graphs)]
@@ -676,11 +685,15 @@ def main():
     else:
         for _ in range(args.steps):
             step(True)
+    for k in range(S):
+        tev[k][1].record(streams[k])
     t_enq = time.perf_counter() - t0             # host time to enqueue the timed steps
     torch.cuda.synchronize(dev)
     barrier(ws)
     torch.cuda.synchronize(dev)
     el_rank = time.perf_counter() - t0
+    # device span of the timed region: first shard start to last shard end
+    dev_span_ms = max(tev[0][0].elapsed_time(tev[k][1]) for k in range(S))
     if graphs:
         # the roofline's kernel time: HIP events around bgx_step in eager steps right
         # after the timed replays (events cannot be timed inside a graph)
@@ -743,25 +756,38 @@ def main():
                                "one wave per game, "
                                + ("the light launch on the engine's side stream (event fork-join)" if args.fork_steps
                                   else "both launches on the shard's stream")
-                               + "; HIP events around bgx_step on the shard's stream, per shard of "
-                                 "games_per_gpu/shards lanes",
-                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": f"bytes per env-step launch (one shard of {Bs} lanes)",
+                               + f"; {S} shards' steps overlap on {S} streams",
+                     "bound": "hbm", "achieved": B * bytes_per_lane / (dev_span_ms / args.steps * 1e-3) / 1e9,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": B * bytes_per_lane / (dev_span_ms / args.steps * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "window": "the timed region on the device clock (HIP events on every shard's stream before the "
+                               "first and after the last timed step) / steps: the shards' env-step launches overlap "
+                               "each other and the policy kernels, so the step window is the launches' union",
+                     "window_ms": dev_span_ms / args.steps, "algorithmic_bytes_per_step": B * bytes_per_lane,
+                     "traffic": traffic * S if traffic else None,
+                     "traffic_unit": f"bytes per env step of all {S} shards (PMC, profiles/latest_summary.json)",
                      "traffic_per_lane_step": traffic / Bs if traffic else None,
                      "traffic_over_algorithmic": traffic / (Bs * bytes_per_lane) if traffic else None,
-                     "traffic_source": traffic_src, "algorithmic_bytes_per_step": Bs * bytes_per_lane, "lanes_per_launch": Bs,
-                     "kernel_ms": kern_ms, "bytes_per_lane_step": bytes_per_lane,
+                     "traffic_source": traffic_src, "lanes_per_step": B, "bytes_per_lane_step": bytes_per_lane,
+                     "mean_legal_moves": mean_moves,
+                     "per_shard_eager": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS, "kernel_ms": kern_ms,
+                                         "lanes_per_launch": Bs, "algorithmic_bytes_per_step": Bs * bytes_per_lane,
+                                         "note": "one shard's env-step bytes / HIP events around its bgx_step in 16 "
+                                                 "eager steps right after the timed region, the other shards' "
+                                                 "kernels sharing the GPU"},
                      "rocprof_avg_us": prof_kernels,
-                     "mean_legal_moves": mean_moves},
+                     "rocprof_note": "per-launch averages of the C3 step's kernels from the committed kernel trace "
+                                     "(profiles/latest_summary.json env_step); under 4-shard overlap a launch's "
+                                     "duration includes the time it shares the CUs with the other shards"},
     }
     # the same bytes chip-wide: every shard's env-step bytes over the whole step window
     # (ms_per_step), while the per-shard figure above divides one shard's bytes by one
     # shard's event window with the other shards' kernels sharing the GPU
     ms_step = el * 1e3 / args.steps
     chip = B * bytes_per_lane / (ms_step * 1e-3) / 1e9
-    line["roofline"]["chip_wide"] = {"achieved": chip, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                     "frac": chip / HBM_PEAK_GBS, "algorithmic_bytes_per_step": B * bytes_per_lane,
-                                     "window_ms": ms_step, "note": "all shards' algorithmic env-step bytes / ms_per_step"}
+    line["roofline"]["chip_wide_wall"] = {"achieved": chip, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                          "frac": chip / HBM_PEAK_GBS, "window_ms": ms_step,
+                                          "note": "all shards' algorithmic env-step bytes / ms_per_step (host clock)"}
     line["host_enqueue_ms"] = t_enq * 1e3
     line["per_rank"] = [{"rank": k, "env_steps": r[0], "seconds": r[1]} for k, r in enumerate(per_rank)]
     if backend is not None:
@@ -848,11 +874,11 @@ def main():
                                                   (summ or {}).get("pmc_command") if prof_ok else None)
     if sq and sq.get("instructions_per_lane_step") and args.workload == "c3":
         line["roofline_issue"] = issue_roofline(sq, Bs, kern_ms, summ.get("pmc_command"))
-        # chip-wide: every lane-step of the whole GPU over ms_per_step (the per-CU scalar
-        # unit's real load; the object above prices one shard over its own event window)
-        cw = issue_roofline(sq, B, el * 1e3 / args.steps, summ.get("pmc_command"))
+        # chip-wide: every lane-step of the whole GPU over the device step window (the per-CU
+        # scalar unit's real load; the object above prices one shard over its own event window)
+        cw = issue_roofline(sq, B, dev_span_ms / args.steps, summ.get("pmc_command"))
         line["roofline_issue"]["chip_wide"] = {k: cw[k] for k in ("pipe", "achieved", "peak", "unit", "frac", "pipes")}
-        line["roofline_issue"]["chip_wide"]["window_ms"] = el * 1e3 / args.steps
+        line["roofline_issue"]["chip_wide"]["window_ms"] = dev_span_ms / args.steps
     if args.two_ply_batches > 0:
         eng2 = engs[0] if S == 1 else bgx.Engine(batch=B, max_moves=500, seed=77 + rank, dice="philox",
                                                  auto_reset=True, device=dev)

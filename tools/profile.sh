@@ -20,6 +20,9 @@ mkdir -p $OUT
 PMC_ARGS="--steps 200 --warmup 10 --two-ply-batches 0 --horizon 0 --no-cpu-baseline --c2-steps 0 --mirror-steps 0"
 REGEX='k_step|k_order|k_movegen_over'
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python bench.py "$@" > $OUT/trace.log 2>&1
+# the C3 step alone, kernel trace only: the env-step kernels' durations over the timed window
+export C3TRACE_ARGS="--steps 200 --warmup 10 --two-ply-batches 0 --horizon 0 --no-cpu-baseline --c2-steps 0 --mirror-steps 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/c3trace -o run -- python bench.py $C3TRACE_ARGS > $OUT/c3trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$REGEX" --output-format csv -d $OUT/fetch -o run -- python bench.py $PMC_ARGS > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$REGEX" --output-format csv -d $OUT/write -o run -- python bench.py $PMC_ARGS > $OUT/write.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM SQ_INSTS_BRANCH --kernel-include-regex "$REGEX" --output-format csv -d $OUT/sqi -o run -- python bench.py $PMC_ARGS > $OUT/sqi.log 2>&1

@@ -88,6 +88,34 @@ for k in kernels:
         env["busy_ns_per_step"] += k.get("avg_ns_c3", k["avg_ns"])
         env["hbm_bytes_per_step"] += k.get("hbm_bytes_per_launch") or 0.0
 
+# The C3 step's kernels over the timed window of a C3-only kernel trace (the "c3trace"
+# pass: bench.py --steps K, C3 only): the timed replays are the K x shards policy
+# dispatches before the 16 x shards eager steps that follow the timed region; each
+# kernel's average launch duration over that window (the roofline's rocprof figure).
+c3t = os.path.join(out, "c3trace", "run_kernel_trace.csv")
+if os.path.exists(c3t):
+    rows = sorted(csv.DictReader(open(c3t)), key=lambda r: int(r["Start_Timestamp"]))
+    a3 = os.environ.get("C3TRACE_ARGS", "--steps 200").split()
+    K3 = int(a3[a3.index("--steps") + 1])
+    S3 = int(a3[a3.index("--shards") + 1]) if "--shards" in a3 else 4
+    pol = [i for i, r in enumerate(rows) if "k_policy_act" in r["Kernel_Name"]]
+    if len(pol) >= (16 + K3) * S3:
+        lo, hi = pol[-(16 + K3) * S3], pol[-16 * S3]
+        win = rows[lo:hi]
+        per = {}
+        for r in win:
+            per.setdefault(short(r["Kernel_Name"]), []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        t0 = int(win[0]["Start_Timestamp"]); t1 = max(int(r["End_Timestamp"]) for r in win)
+        env["timed_window"] = {"steps": K3, "shards": S3, "span_ms_per_step": (t1 - t0) / 1e6 / K3,
+                               "kernels": {n: {"launches": len(d), "avg_us": statistics.mean(d) / 1e3}
+                                           for n, d in sorted(per.items(), key=lambda x: -sum(x[1]))},
+                               "command": "python bench.py " + " ".join(a3)}
+        for k in env["kernels"]:
+            w = env["timed_window"]["kernels"].get(k["name"])
+            if w:
+                k["avg_ns"] = w["avg_us"] * 1e3
+                k["avg_source"] = "c3trace timed window"
+
 # SQ passes of the C3 step alone ("sqi": instruction counts, "sqc": wave-cycle split).
 # Both passes run the same command, so per-pass totals over all env-step dispatches /
 # the lane-steps of that run give per-lane-step figures; the lane-steps are counted as
