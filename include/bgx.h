@@ -388,15 +388,19 @@ int bgx_lane_returns(const float* rewards_dev, const uint8_t* dones_dev, int32_t
  * the parameters' gradients from the accumulators times post (fp32): fc1 weight = gw1[:,
  * :198], bias = gw1[:, 198], action_head = gw2[:A], gb2[:A], value_head = gw2[A], gb2[A];
  * with guard_dev (uint8, may be NULL) also guard |= 2 (max_a |W2h[a]| sqrt(hmax2[0]) +
- * max_a |b2h[a]|) > limit over a < A from prep's bound (the fused head's masked-action bound). */
+ * max_a |b2h[a]|) > limit over a < A from prep's bound (the fused head's masked-action bound).
+ * Loss parts (both may be NULL): prep zeroes sums_dev [3] (fp64, the epoch's loss sums that
+ * bgx_ppo_rows adds to); grads adds (m0, m1, m2, m0 + c_value m1 - c_entropy m2), m = sums /
+ * n_total, to parts_dev [4] in fp64 (the torch form's arithmetic, no contraction). */
 int bgx_ppo_epoch_prep(const float* w1_dev, const float* b1_dev, const float* wa_dev, const float* ba_dev,
                        const float* wv_dev, const float* bv_dev, int32_t hidden, int32_t n_actions, void* w1pack_dev,
                        void* b1h_dev, void* w2h_dev, void* b2h_dev, float* gw1_dev, float* gw2_dev, float* gb2_dev,
-                       float* hmax2_dev_or_null, float* bound_dev_or_null, void* stream);
+                       float* hmax2_dev_or_null, float* bound_dev_or_null, double* sums_dev_or_null, void* stream);
 int bgx_ppo_epoch_grads(const float* gw1_dev, const float* gw2_dev, const float* gb2_dev, int32_t hidden,
                         int32_t n_actions, float post, float* w1_grad, float* b1_grad, float* wa_grad, float* ba_grad,
                         float* wv_grad, float* bv_grad, const float* bound_dev, const float* hmax2_dev,
-                        float limit, uint8_t* guard_dev_or_null, void* stream);
+                        float limit, uint8_t* guard_dev_or_null, const double* sums_dev, double n_total,
+                        double c_value, double c_entropy, double* parts_dev_or_null, void* stream);
 
 /* The episode accounting of a [T][B] rollout (the reference driver's per-env loop,
  * train.py:55-99; bgx.train.episode_stats): records_dev uint8[T][B][64] (the mover is

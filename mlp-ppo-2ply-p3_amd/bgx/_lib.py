@@ -75,9 +75,10 @@ SIGNATURES = {
     "bgx_host_device_ptr": (ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     "bgx_lane_returns": (ctypes.c_int, [_P, _P, _I32, _I32, ctypes.c_float, _P, _P]),
     "bgx_ppo_epoch_prep": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                          _P]),
+                                          _P, _P]),
     "bgx_ppo_epoch_grads": (ctypes.c_int, [_P, _P, _P, _I32, _I32, ctypes.c_float, _P, _P, _P, _P, _P, _P, _P, _P,
-                                           ctypes.c_float, _P, _P]),
+                                           ctypes.c_float, _P, _P, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                           _P, _P]),
     "bgx_episode_stats_workspace": (ctypes.c_int64, [_I32]),
     "bgx_episode_stats": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _P, _P, _P]),
     "bgx_adam_step": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.c_double, ctypes.c_double,

@@ -16,6 +16,7 @@ which invalidates the capture.
 """
 from __future__ import annotations
 
+import gc
 import os
 import sys
 
@@ -34,6 +35,12 @@ def capture(site: str, body, stream: torch.cuda.Stream) -> torch.cuda.CUDAGraph:
     so another thread's event queries, e.g. an RCCL watchdog's, cannot invalidate
     it).  On any failure: message on stderr, then os._exit(EXIT_CAPTURE_FAILED)."""
     g = torch.cuda.CUDAGraph()
+    # no cyclic garbage collection while capturing: torch.cuda.graph collects before the
+    # capture starts, but a collection triggered inside it would run finalizers (stream,
+    # event and graph destructors of earlier captures) that HIP refuses mid-capture -- an
+    # abort, not an exception (round 6: a recapture inside PPOTrainer.update)
+    gc_was = gc.isenabled()
+    gc.disable()
     try:
         with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
             body()
@@ -45,4 +52,7 @@ def capture(site: str, body, stream: torch.cuda.Stream) -> torch.cuda.CUDAGraph:
                          "stream may still be capturing; exiting (no eager continuation)\n")
         sys.stderr.flush()
         os._exit(EXIT_CAPTURE_FAILED)
+    finally:
+        if gc_was:
+            gc.enable()
     return g

@@ -213,22 +213,23 @@ class _PPOHead(torch.autograd.Function):
 
 def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_coef: float, group=None,
               amp: bool = True, fused: bool | None = None, step: bool = True, sync: bool = True, guard=None,
-              fused_head: bool = True, scale_hint=None):
+              fused_head: bool = True, scale_hint=None, parts=None):
     """One full-batch PPO epoch (ppo_agent.py:268-305) over `chunks` =
     iterable of (features, legal_mask, actions, old_logp, returns, advantages
     [, records]), with gradient accumulation and one all-reduce.  Returns loss
-    parts.  fused (default: on the GPU when the chunks carry their 64-byte
+    parts (sync=False with `parts` given: added on the device to that fp64 [4] tensor, which
+    is returned).  fused (default: on the GPU when the chunks carry their 64-byte
     records): the loss head runs as one HIP kernel (bgx_ppo_head) instead of the
     torch formulation below, which stays as its reference (tests compare them)."""
     optimizer.zero_grad(set_to_none=True)
-    parts = torch.zeros(4, dtype=torch.float64)
+    acc = torch.zeros(4, dtype=torch.float64)
     dev = next(net.parameters()).device
     dev_type = dev.type
     if fused is None:
         fused = dev_type == "cuda"
     if fused:
         return _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync, guard,
-                                fused_head, scale_hint)
+                                fused_head, scale_hint, parts)
     for feats, legal, actions, old_logp, returns, adv, *_ in chunks:
         w = feats.shape[0] / n_total
         with autocast(device_type=dev_type, enabled=amp):
@@ -246,13 +247,13 @@ def ppo_epoch(net: nn.Module, optimizer, scaler, chunks, n_total: int, entropy_c
             entropy = dist_.entropy().mean()
             loss = policy_loss + VALUE_LOSS_COEF * value_loss - entropy_coef * entropy
         scaler.scale(loss * w).backward()
-        parts += torch.tensor([policy_loss.item(), value_loss.item(), entropy.item(), loss.item()],
-                              dtype=torch.float64) * w
+        acc += torch.tensor([policy_loss.item(), value_loss.item(), entropy.item(), loss.item()],
+                            dtype=torch.float64) * w
     if step:
         allreduce_mean_([p.grad for p in net.parameters() if p.grad is not None], group)
         scaler.step(optimizer)
         scaler.update()
-    return parts
+    return acc
 
 
 PPO_COLSUM_BLOCKS = 2048       # include/bgx.h BGX_PPO_COLSUM_BLOCKS
@@ -464,7 +465,15 @@ def _ptr_or_none(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
-def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
+def _fused_fast(net) -> bool:
+    """The fused epoch's one-launch prologue / epilogue apply (bgx_ppo_epoch_prep / _grads):
+    198 input features and fp32 contiguous parameters."""
+    params = (net.fc1.weight, net.fc1.bias, net.action_head.weight, net.action_head.bias, net.value_head.weight,
+              net.value_head.bias)
+    return net.fc1.weight.shape[1] == 198 and all(t.dtype == torch.float32 and t.is_contiguous() for t in params)
+
+
+def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None, parts=None, entropy_coef=0.0):
     """The fp16-autocast epoch with the output layer and loss head fused
     (bgx_ppo_rows + bgx_ppo_gw2): fc1 from the records (bgx_fc1_records), then per
     row the logits, the loss head, dy and dh = ReLU'(h) fp16(dy W2h) on MFMA without
@@ -473,7 +482,10 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
     no feature rows in HBM).  Same fp16 operands, fp32 accumulation and per-row
     gradient scaling as _ppo_epoch_amp_manual; gradients land in p.grad as fp32.
     The chunks' feature entries are not read.  `guard` (a device bool, optional) is
-    set when the masked-action shortcut's bound (MASK_SHORTCUT_LIMIT) does not hold."""
+    set when the masked-action shortcut's bound (MASK_SHORTCUT_LIMIT) does not hold.
+    `parts` (fp64 [4], fast path only): the prologue zeroes `sums` and the epilogue adds this
+    epoch's loss parts to `parts` (the torch form's arithmetic), so no small torch kernels run
+    around the epoch."""
     eps, c_v, c_e, gscale = coefs
     row_scale = gscale * n_total / min(n_total, REF_ROWS)
     post = min(n_total, REF_ROWS) / n_total
@@ -487,7 +499,9 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
     params = (W1, b1, Wa, ba, wv, bv)
     # one launch for the casts, the packed fc1 fragments and the zeroed accumulators (and
     # one for the gradient hand-off below) instead of ~20 small torch kernels per epoch
-    fast = F_in == 198 and all(t.dtype == torch.float32 and t.is_contiguous() for t in params)
+    fast = _fused_fast(net)
+    if parts is not None and not fast:
+        raise ValueError("loss-part accumulation needs the fast fused epoch")
     with torch.no_grad():
         L = _lib.load()
         p = lambda t: ctypes.c_void_p(t.data_ptr())
@@ -503,7 +517,8 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
             hmax2 = torch.empty(1, dtype=torch.float32, device=dev) if guard is not None else None
             bound = torch.empty(2, 512, dtype=torch.float32, device=dev) if guard is not None else None
             check(L.bgx_ppo_epoch_prep(*[p(t) for t in params], Hd, A, p(w1pack), p(b1h), p(W2h), p(b2h), p(gW1),
-                                       p(gW2), p(gb2), _ptr_or_none(hmax2), _ptr_or_none(bound), stream),
+                                       p(gW2), p(gb2), _ptr_or_none(hmax2), _ptr_or_none(bound),
+                                       _ptr_or_none(sums if parts is not None else None), stream),
                   "bgx_ppo_epoch_prep")
         else:
             W1h, b1h = W1.half(), b1.half()
@@ -544,7 +559,8 @@ def _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard=None):
             grads = [torch.empty_like(t) for t in params]
             check(L.bgx_ppo_epoch_grads(p(gW1), p(gW2), p(gb2), Hd, A, float(post), *[p(g) for g in grads],
                                         _ptr_or_none(bound), _ptr_or_none(hmax2), float(MASK_SHORTCUT_LIMIT),
-                                        _ptr_or_none(guard), stream), "bgx_ppo_epoch_grads")
+                                        _ptr_or_none(guard), p(sums), float(n_total), float(VALUE_LOSS_COEF),
+                                        float(entropy_coef), _ptr_or_none(parts), stream), "bgx_ppo_epoch_grads")
             W1.grad, b1.grad, Wa.grad, ba.grad, wv.grad, bv.grad = grads
             return
         if post != 1.0:
@@ -608,7 +624,7 @@ def adam_step(optimizer, scaler) -> bool:
 
 
 def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, group, amp, step, sync=True, guard=None,
-                     fused_head=True, scale_hint=None):
+                     fused_head=True, scale_hint=None, parts=None):
     """scale_hint (PPOTrainer.update): {"scale", "tracker"}, the host's copy of the
     GradScaler state, used instead of get_scale() (a host sync per epoch that left the
     GPU idle while the next epoch's launches were issued) and advanced as a finite
@@ -617,16 +633,24 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
     (non-finite) step made them differ."""
     dev = next(net.parameters()).device
     if scaler.is_enabled():
-        scaler.scale(torch.ones((), device=dev))          # initialises the scale tensor lazily
+        if getattr(scaler, "_scale", None) is None:
+            scaler.scale(torch.ones((), device=dev))      # initialises the scale tensor lazily
         scale = scale_hint["scale"] if scale_hint is not None else scaler.get_scale()
     else:
         scale = 1.0
-    sums = torch.zeros(3, dtype=torch.float64, device=dev)
     coefs = (EPS_CLIP, VALUE_LOSS_COEF, float(entropy_coef), float(scale) / n_total)
     manual = amp and _is_policy_mlp(net)
+    # `parts` (fp64 [4] accumulator, sync=False only): the fast fused epoch adds its loss parts
+    # on the device inside its own epilogue launch (and its prologue zeroes the sums)
+    in_kernel = (parts is not None and not sync and manual and fused_head and _fused_head_ok(net)
+                 and _fused_fast(net))
+    if in_kernel and (parts.device != dev or parts.dtype != torch.float64 or parts.numel() != 4):
+        raise ValueError("parts must be a float64 [4] tensor on the parameters' device")
+    sums = (torch.empty if in_kernel else torch.zeros)(3, dtype=torch.float64, device=dev)
     if manual:
         if fused_head and _fused_head_ok(net):
-            _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard)
+            _ppo_epoch_amp_fused(net, chunks, n_total, coefs, sums, guard, parts=parts if in_kernel else None,
+                                 entropy_coef=entropy_coef)
         else:
             _ppo_epoch_amp_manual(net, chunks, n_total, coefs, sums)
         chunks = ()
@@ -649,8 +673,14 @@ def _ppo_epoch_fused(net, optimizer, scaler, chunks, n_total, entropy_coef, grou
                 t = 0
             scale_hint["tracker"] = t
     if not sync:        # loss parts stay on the device (fp64, same arithmetic): no host sync per epoch
+        if in_kernel:
+            return parts
         m = sums / n_total
-        return torch.cat([m, (m[0] + VALUE_LOSS_COEF * m[1] - entropy_coef * m[2]).reshape(1)])
+        e = torch.cat([m, (m[0] + VALUE_LOSS_COEF * m[1] - entropy_coef * m[2]).reshape(1)])
+        if parts is not None:
+            parts += e
+            return parts
+        return e
     pol, val, ent = (sums / n_total).tolist()
     tot = pol + VALUE_LOSS_COEF * val - entropy_coef * ent
     return torch.tensor([pol, val, ent, tot], dtype=torch.float64)
@@ -1005,12 +1035,13 @@ class PPOTrainer:
                     f, legal = features_and_masks(recs[s:e], self.A)
                 yield f, legal, acts[s:e], old[s:e], R[s:e], adv[s:e], recs[s:e], preps[i]
 
-        parts = None
+        parts = torch.zeros(4, dtype=torch.float64, device=self.dev)
         for _ in range(NUM_EPOCHS):
-            e = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
-                          amp=self.amp, fused=self.fused, sync=False, guard=guard, fused_head=fused_head,
-                          scale_hint=scale_hint)
-            parts = e if parts is None else parts + e
+            e = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group, amp=self.amp,
+                          fused=self.fused, sync=False, guard=guard, fused_head=fused_head, scale_hint=scale_hint,
+                          parts=parts)
+            if e is not parts:                 # the torch epoch returns its own (host) parts
+                parts += e.to(parts.device)
         return parts
 
     def _epochs_graphed(self, recs, acts, old, R, adv, guard, hint):
@@ -1042,7 +1073,9 @@ class PPOTrainer:
                 _, plan, row_plan = c["plan"]
                 yield None, None, aa, oo, RR, dd, rr, {"plan": (None, plan, row_plan)}
 
-        parts = None
+        if getattr(self, "_uparts", None) is None:
+            self._uparts = torch.zeros(4, dtype=torch.float64, device=self.dev)
+        self._uparts.zero_()                   # the captured epochs add their loss parts to it
         cur = torch.cuda.current_stream(self.dev)
         for _ in range(NUM_EPOCHS):
             key = self._ugraph_key(hint["scale"], N)
@@ -1056,20 +1089,18 @@ class PPOTrainer:
                 def body():
                     out["e"] = ppo_epoch(self.net, self.opt, self.scaler, chunks(), N, self.entropy_coef, self.group,
                                          amp=self.amp, fused=self.fused, sync=False, guard=guard, fused_head=True,
-                                         scale_hint=dict(hint))
+                                         scale_hint=dict(hint), parts=self._uparts)
                 g = capture("ppo_update", body, st)
                 cur.wait_stream(st)
                 self._ugraph = (key, g, out["e"])
             self._ugraph[1].replay()
-            e = self._ugraph[2]
-            parts = e.clone() if parts is None else parts + e
             if self.scaler.is_enabled():         # as _ppo_epoch_fused advances its scale_hint
                 t = hint["tracker"] + 1
                 if t == self.scaler._growth_interval:
                     hint["scale"] = float(np.float32(hint["scale"] * self.scaler._growth_factor))
                     t = 0
                 hint["tracker"] = t
-        return parts
+        return self._uparts.clone()
 
     def _snapshot_tensors(self):
         ts = [p for p in self.net.parameters()]

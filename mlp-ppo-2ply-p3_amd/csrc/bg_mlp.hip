@@ -739,6 +739,7 @@ struct EpochPrep {
     _Float16 *b1h, *w2h, *b2h;
     float *gw1, *gw2, *gb2, *hmax2;
     float* bound;        // [2][512]: |fp16(action row a)| and |fp16(action bias a)| (may be NULL)
+    double* sums;        // the epoch's 3 fp64 loss sums, zeroed (may be NULL)
 };
 __global__ __launch_bounds__(256) void k_ppo_epoch_prep(EpochPrep a) {
     const int H = a.hidden, A = a.n_actions;
@@ -791,6 +792,7 @@ __global__ __launch_bounds__(256) void k_ppo_epoch_prep(EpochPrep a) {
             a.hmax2[0] = 0.0f;
         }
     }
+    if (a.sums && blockIdx.x == 0 && threadIdx.x < 3) a.sums[threadIdx.x] = 0.0;
 }
 
 __global__ void k_counter_add(uint32_t* ctr, uint32_t v) {
@@ -908,14 +910,14 @@ int bgx_fc1_pack(const void* w1h_dev, int32_t hidden, void* packed_dev, void* st
 int bgx_ppo_epoch_prep(const float* w1_dev, const float* b1_dev, const float* wa_dev, const float* ba_dev,
                        const float* wv_dev, const float* bv_dev, int32_t hidden, int32_t n_actions, void* w1pack_dev,
                        void* b1h_dev, void* w2h_dev, void* b2h_dev, float* gw1_dev, float* gw2_dev, float* gb2_dev,
-                       float* hmax2_dev_or_null, float* bound_dev_or_null, void* stream) {
+                       float* hmax2_dev_or_null, float* bound_dev_or_null, double* sums_dev_or_null, void* stream) {
     if (bgx_fc1_packed_size(hidden) < 0 || n_actions <= 0 || n_actions >= 512) return BGX_EINVAL;
     if (!w1_dev || !b1_dev || !wa_dev || !ba_dev || !wv_dev || !bv_dev || !w1pack_dev || !b1h_dev || !w2h_dev ||
         !b2h_dev || !gw1_dev || !gw2_dev || !gb2_dev || (uintptr_t)w1pack_dev % 16)
         return BGX_EINVAL;
     EpochPrep a{w1_dev, b1_dev, wa_dev, ba_dev, wv_dev, bv_dev, hidden, n_actions, (hidden + 31) / 32,
                 (uint4*)w1pack_dev, (_Float16*)b1h_dev, (_Float16*)w2h_dev, (_Float16*)b2h_dev, gw1_dev, gw2_dev,
-                gb2_dev, hmax2_dev_or_null, bound_dev_or_null};
+                gb2_dev, hmax2_dev_or_null, bound_dev_or_null, sums_dev_or_null};
     hipLaunchKernelGGL(k_ppo_epoch_prep, dim3(512), dim3(256), 0, (hipStream_t)stream, a);
     return hipGetLastError() == hipSuccess ? BGX_OK : BGX_EDEVICE;
 }

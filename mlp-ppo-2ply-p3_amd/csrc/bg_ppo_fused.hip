@@ -1330,9 +1330,26 @@ struct EpochGrads {
     float limit;
     uint8_t* guard;
     const float* bound;         // [2][512] from bgx_ppo_epoch_prep
+    const double* sums;         // the epoch's loss sums (may be NULL: no parts)
+    double n_total, c_value, c_entropy;
+    double* parts;              // [4] += (policy, value, entropy, total) of this epoch
 };
 __global__ __launch_bounds__(256) void k_ppo_epoch_grads(EpochGrads a) {
     const int H = a.hidden, A = a.n_actions;
+    if (a.parts && blockIdx.x == gridDim.x - 1) {
+        // the epoch's loss parts as the torch form computes them (fp64, no contraction):
+        // m = sums / n; total = m0 + c_v m1 - c_e m2; parts += (m0, m1, m2, total)
+        if (threadIdx.x == 0) {
+            const double m0 = __ddiv_rn(a.sums[0], a.n_total), m1 = __ddiv_rn(a.sums[1], a.n_total),
+                         m2 = __ddiv_rn(a.sums[2], a.n_total);
+            const double tot = __dsub_rn(__dadd_rn(m0, __dmul_rn(a.c_value, m1)), __dmul_rn(a.c_entropy, m2));
+            a.parts[0] = __dadd_rn(a.parts[0], m0);
+            a.parts[1] = __dadd_rn(a.parts[1], m1);
+            a.parts[2] = __dadd_rn(a.parts[2], m2);
+            a.parts[3] = __dadd_rn(a.parts[3], tot);
+        }
+        return;
+    }
     if (blockIdx.x == 0 && a.guard) {
         __shared__ float mn[256], mb[256];
         float n2 = 0.0f, b = 0.0f;
@@ -1358,7 +1375,7 @@ __global__ __launch_bounds__(256) void k_ppo_epoch_grads(EpochGrads a) {
     }
     const long long n0 = (long long)H * 198, n1 = n0 + H, n2 = n1 + (long long)A * H, n3 = n2 + A, n4 = n3 + H,
                     n5 = n4 + 1;
-    const int nb = a.guard ? gridDim.x - 1 : gridDim.x, b0 = a.guard ? blockIdx.x - 1 : blockIdx.x;
+    const int nb = (int)gridDim.x - (a.guard ? 1 : 0) - (a.parts ? 1 : 0), b0 = a.guard ? blockIdx.x - 1 : blockIdx.x;
     for (long long g = (long long)b0 * 256 + threadIdx.x; g < n5; g += (long long)nb * 256) {
         if (g < n0) {
             const int u = (int)(g / 198), f = (int)(g % 198);
@@ -1381,14 +1398,19 @@ __global__ __launch_bounds__(256) void k_ppo_epoch_grads(EpochGrads a) {
 extern "C" int bgx_ppo_epoch_grads(const float* gw1_dev, const float* gw2_dev, const float* gb2_dev, int32_t hidden,
                                    int32_t n_actions, float post, float* w1_grad, float* b1_grad, float* wa_grad,
                                    float* ba_grad, float* wv_grad, float* bv_grad, const float* bound_dev,
-                                   const float* hmax2_dev, float limit, uint8_t* guard_dev_or_null, void* stream) {
+                                   const float* hmax2_dev, float limit, uint8_t* guard_dev_or_null,
+                                   const double* sums_dev, double n_total, double c_value, double c_entropy,
+                                   double* parts_dev_or_null, void* stream) {
     if (hidden <= 0 || hidden > 128 || n_actions <= 0 || n_actions >= 512) return BGX_EINVAL;
     if (!gw1_dev || !gw2_dev || !gb2_dev || !w1_grad || !b1_grad || !wa_grad || !ba_grad || !wv_grad || !bv_grad)
         return BGX_EINVAL;
     if (guard_dev_or_null && (!bound_dev || !hmax2_dev)) return BGX_EINVAL;
+    if (parts_dev_or_null && (!sums_dev || !(n_total > 0.0))) return BGX_EINVAL;
     EpochGrads a{gw1_dev, gw2_dev, gb2_dev, hidden, n_actions, post, w1_grad, b1_grad, wa_grad, ba_grad, wv_grad,
-                 bv_grad, hmax2_dev, limit, guard_dev_or_null, bound_dev};
-    hipLaunchKernelGGL(k_ppo_epoch_grads, dim3(guard_dev_or_null ? 257 : 256), dim3(256), 0, (hipStream_t)stream, a);
+                 bv_grad, hmax2_dev, limit, guard_dev_or_null, bound_dev, sums_dev, n_total, c_value, c_entropy,
+                 parts_dev_or_null};
+    hipLaunchKernelGGL(k_ppo_epoch_grads, dim3(256 + (guard_dev_or_null ? 1 : 0) + (parts_dev_or_null ? 1 : 0)),
+                       dim3(256), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }
