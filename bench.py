@@ -442,9 +442,24 @@ def two_ply_bench(engs, batches: int, ws: int, dev, hidden: int = 40, streams=No
                          "bound": "mfma", "achieved": eval_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": eval_tflops / BF16_PEAK_TFLOPS if eval_tflops else None,
                          "flop_per_leaf": flop_per_leaf,
-                         "issued_over_algorithmic": 2 * (units / hidden) * (208 / 198),
-                         "note": f"issued MFMA work = algorithmic x 2 (W1 hi+lo for fp32 accuracy) x "
-                                 f"{units}/{hidden} ({tiles}) x 208/198 (K padding, bias as a feature)"}}
+                         "issued_over_algorithmic": _issued_over_algorithmic(nt, leaves_all / roots, flop_per_leaf),
+                         "issued_unfactored_bound": 2 * (units / hidden) * (208 / 198),
+                         "note": f"issued_over_algorithmic: SQ_INSTS_MFMA of a whole-batch k_eval<{nt}> dispatch "
+                                 "(profiles/latest_summary.json) x 32,768 FLOP per v_mfma_f32_32x32x16_f16 / (65,536 "
+                                 "roots x leaves per root x FLOP per leaf); the factored evaluator runs 7 + (hit "
+                                 "blocks) of the 13 k-blocks per leaf.  issued_unfactored_bound: algorithmic x 2 (W1 "
+                                 f"hi+lo for fp32 accuracy) x {units}/{hidden} ({tiles}) x 208/198 (K padding, bias)"}}
+
+
+def _issued_over_algorithmic(nt: int, leaves_per_root: float, flop_per_leaf: int):
+    """Issued / algorithmic MFMA FLOPs of k_eval<nt> from the committed PMC pass (None
+    without one): its largest dispatch is one engine's whole 65,536-root batch."""
+    try:
+        summ = json.load(open(os.path.join(ROOT, "profiles", "latest_summary.json")))
+        e = next(x for x in summ.get("two_ply_eval", []) if x["kernel"] == f"k_eval<{nt}>")
+        return e["SQ_INSTS_MFMA_max_dispatch"] * 32768 / (65536 * leaves_per_root * flop_per_leaf)
+    except Exception:
+        return None
 
 
 EVAL_PMC_ARGS = ("--steps 2 --warmup 1 --burn-in 150 --horizon 0 --no-cpu-baseline --two-ply-batches 1 "

@@ -196,6 +196,8 @@ for k in kernels:
               "SQ_INSTS_LDS", "SQ_INSTS_SALU"):
         if c in m:
             e[c] = statistics.mean(m[c])
+    if "SQ_INSTS_MFMA" in m:      # the largest dispatch = one whole 65,536-root batch (one engine)
+        e["SQ_INSTS_MFMA_max_dispatch"] = max(m["SQ_INSTS_MFMA"])
     if "SQ_INSTS_VALU" in e:      # VALU pipe busy (2 cycles per wave64 instruction, MFMA included)
         e["valu_issue_frac_at_2p4GHz"] = e["SQ_INSTS_VALU"] * 2 / (SIMDS * k["avg_ns"] * CLOCK_GHZ)
     f = erows.get(k["name"], {}).get("FETCH_SIZE")
