@@ -296,10 +296,14 @@ void k_ppo_rows(RowsArgs a, const int32_t* __restrict__ range) {
                 }                                                                 \
             }                                                                     \
         }
+// The small variants' rows have lim <= 32 TM <= 128, so the value tile's action columns
+// (480-499) are never in play: tz = -inf there, p = 0, and every pass below would add exact
+// zeros (round 6: the passes skip it; its dz is gv at the value column, zero elsewhere).
+#define BGX_TILE_SM(k) (BGX_TILE_ON(k) && !(kKeep && (k) == kVk))
 #define BGX_FOR_ELEM(BODY)                                                        \
         BGX_LAUNDER_Z()                                                           \
         _Pragma("unroll") for (int k = 0; k < C::kImg; ++k) {                     \
-            if (BGX_TILE_ON(k)) {                                                 \
+            if (BGX_TILE_SM(k)) {                                                 \
                 const int lt = lim - 32 * BGX_TILE_T(k) - 4 * hh;                 \
                 const int at = act - 32 * BGX_TILE_T(k) - 4 * hh;                 \
                 (void)at;                                                         \
@@ -365,10 +369,15 @@ void k_ppo_rows(RowsArgs a, const int32_t* __restrict__ range) {
                     for (int e2 = 0; e2 < 2; ++e2) {
                         const int ii = i + e2;
                         const int ko = (ii & 3) + 8 * (ii >> 2);
-                        const float tz = kKeep ? TZ[kKeep ? k : 0][ii]
-                            : (ko < lt ? (float)Z[kKeep ? 0 : k][ii >> 1][ii & 1] * kL2e : -INFINITY);
-                        const Elem e = elem(tz, lse2, nlse);
-                        float d = fmaf(e.p, fmaf(k1, e.q, k2), ko == at ? gla : 0.0f);
+                        float d;
+                        if (kKeep && k == kVk) {      // out of play: p = 0 (an out-of-play act keeps gla = 0)
+                            d = ko == at ? gla : 0.0f;
+                        } else {
+                            const float tz = kKeep ? TZ[kKeep ? k : 0][ii]
+                                : (ko < lt ? (float)Z[kKeep ? 0 : k][ii >> 1][ii & 1] * kL2e : -INFINITY);
+                            const Elem e = elem(tz, lse2, nlse);
+                            d = fmaf(e.p, fmaf(k1, e.q, k2), ko == at ? gla : 0.0f);
+                        }
                         if (k == kVk && ii == kVi) d = hh == kVh ? gv : d;
                         d2[e2] = d;
                     }
@@ -440,6 +449,7 @@ void k_ppo_rows(RowsArgs a, const int32_t* __restrict__ range) {
     }
 #undef BGX_FOR_ELEM
 #undef BGX_LAUNDER_Z
+#undef BGX_TILE_SM
 #undef BGX_TILE_ON
 #undef BGX_TILE_T
 #undef BGX_DZ
@@ -569,12 +579,33 @@ __global__ __launch_bounds__(256) void k_ppo_gw2(Gw2Args a) {
         }
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        // the value tile of row tiles whose rows have no action column there in play (every
+        // class but the 16-tile one, lim <= 480): p = 0 on its action columns, so dz is the
+        // value gradient at column kA and zero elsewhere -- no logits needed (round 6)
+        const bool vfast = at == kVT && __ballot((infc >> 16) > 32 * kVT) == 0ull;
+        uint32_t D[8];
+        if (vfast) {
+            #pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                float d2[2];
+                #pragma unroll
+                for (int e2 = 0; e2 < 2; ++e2) {
+                    const int ri = ((i + e2) & 3) + 8 * ((i + e2) >> 2) + 4 * hh;
+                    const float4 st = sst[wv][ri];
+                    const int act = sinf[wv][ri] & 0xFFFF;
+                    const float d = k == kA ? st.w : (k == act ? st.z : 0.0f);
+                    const _Float16 dh16 = (_Float16)d;
+                    gb += (float)dh16;
+                    d2[e2] = (float)dh16;
+                }
+                D[i >> 1] = __builtin_bit_cast(uint32_t, f16x2{(_Float16)d2[0], (_Float16)d2[1]});
+            }
+        } else {
         f32x16 z;
         #pragma unroll
         for (int i = 0; i < 16; ++i) z[i] = 0.0f;
         #pragma unroll
         for (int s = 0; s < 8; ++s) z = __builtin_amdgcn_mfma_f32_32x32x16_f16(as_h8(ha[s]), as_h8(bw[s]), z, 0, 0, 0);
-        uint32_t D[8];
         #pragma unroll
         for (int i = 0; i < 16; i += 2) {
             float d2[2];
@@ -596,6 +627,7 @@ __global__ __launch_bounds__(256) void k_ppo_gw2(Gw2Args a) {
                 d2[e2] = (float)dh16;
             }
             D[i >> 1] = __builtin_bit_cast(uint32_t, f16x2{(_Float16)d2[0], (_Float16)d2[1]});
+        }
         }
         #pragma unroll
         for (int s = 0; s < 2; ++s) {
