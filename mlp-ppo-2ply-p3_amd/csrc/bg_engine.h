@@ -163,7 +163,9 @@ struct Args {
     int32_t* err;
     int B, max_moves, dice_mode, auto_reset, match_length;
     uint32_t key0, key1;
-    uint64_t* stamps;         // diagnostics only (env BGX_STAMPS): [B][2] start/end s_memrealtime
+    uint64_t* stamps;         // diagnostics only (debug option BGX_STAMPS): [B][2] start/end s_memrealtime
+    int cap_mid;              // tier 1's unique-afterstate cap (cap_fast<kLogMid>; tests: BGX_TIER1_CAP)
+    int cap_main;             // bgx_movegen's main-table cap (cap_fast<9>; tests: BGX_MOVEGEN_CAP)
     // dispatch order (Philox mode): each step predicts its lane's next-turn cost class
     // into cls; k_order turns the classes into perm (heaviest first) for the next launch.
     int32_t* perm;            // blockIdx -> lane, or null (identity)

@@ -15,6 +15,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(64) void k_shared_dice(Args A) {
 template <int LOG>
 __global__ __launch_bounds__(64) void k_movegen(const int8_t* boards, const uint8_t* players, const uint8_t* dice,
                                                 int n, int cap, int16_t* nmoves, int32_t* ntotal, uint64_t* moves,
-                                                int32_t* ovf_count, int32_t* ovf_queue) {
+                                                int32_t* ovf_count, int32_t* ovf_queue, int cap_unique) {
     __shared__ uint4 tab[1 << LOG];
     __shared__ uint4 memo[kMemoSlots];
     const int gi = blockIdx.x;
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(64) void k_movegen(const int8_t* boards, const uint
     const int r0 = (int)ufl(dice[2 * gi]), r1 = (int)ufl(dice[2 * gi + 1]);
     int total;
     bool ovf;
-    int nm = run_movegen<LOG>(bv, pl, r0, r1, moves + (size_t)gi * cap, cap, tab, cap_fast<LOG>(), &total, &ovf, memo);
+    int nm = run_movegen<LOG>(bv, pl, r0, r1, moves + (size_t)gi * cap, cap, tab, cap_unique, &total, &ovf, memo);
     if (ovf) {
         if (l == 0) { const int q = atomicAdd(ovf_count, 1); ovf_queue[q] = gi; }
         nm = 0; total = 0;
@@ -242,23 +243,25 @@ __global__ __launch_bounds__(64) void k_movegen(const int8_t* boards, const uint
 }
 
 // Overflow tiers for positions whose dedup set outgrew the main LDS table
-// (cap 7/8 of 2^LOG slots).  Tier 1: the same code with a 4,096-slot (64 KiB)
-// LDS table, fed by queue 1; anything larger (> 3,584 distinct afterstates)
-// moves to queue 2 = tier 2, a 131,072-slot table in HBM per wave.  Every
-// position stays exact.  SRC 0 = engine lanes, 1 = standalone arrays.
+// (cap 7/8 of 2^LOG slots), fed by the overflow queue.  Tier 1: the same code with a
+// 4,096-slot (64 KiB) LDS table; a position with more distinct afterstates (> 3,584)
+// runs again in the same wave on tier 2, a 131,072-slot table in HBM that is the
+// workgroup's own (grid = kSlowWaves tables).  Every position stays exact.  Round 6:
+// one launch of kSlowWaves workgroups for both tiers (was 256 tier-1 workgroups, then a
+// tier-2 launch fed by a second queue): the queue is empty or short on almost every
+// step, so the launch is mostly its own cost.  SRC 0 = engine lanes, 1 = standalone arrays.
 constexpr int kLogMid = 12;
 
-template <int SRC, int TIER>
+template <int SRC>
 __global__ __launch_bounds__(64) void k_movegen_over(Args A, const int8_t* boards, const uint8_t* players,
                                                      const uint8_t* dice, int cap, int16_t* nmoves, int32_t* ntotal,
                                                      uint64_t* moves, uint4* tables) {
     __shared__ uint4 memo[kMemoSlots];
-    __shared__ uint4 lds_tab[TIER == 1 ? (1 << kLogMid) : 1];
-    uint4* tab = TIER == 1 ? lds_tab : tables + ((size_t)blockIdx.x << kLogSlotsSlow);
-    const int count = (int)ufl((uint32_t)A.ovf_count[TIER - 1]);
-    const int32_t* queue = A.ovf_queue + (TIER == 1 ? 0 : A.B);
+    __shared__ uint4 lds_tab[1 << kLogMid];
+    uint4* slow = tables + ((size_t)blockIdx.x << kLogSlotsSlow);
+    const int count = (int)ufl((uint32_t)A.ovf_count[0]);
     for (int q = blockIdx.x; q < count; q += gridDim.x) {
-        const int gi = (int)ufl((uint32_t)queue[q]);
+        const int gi = (int)ufl((uint32_t)A.ovf_queue[q]);
         const int l = lane_id();
         int bv, pl, r0, r1;
         if (SRC == 0) {
@@ -271,16 +274,9 @@ __global__ __launch_bounds__(64) void k_movegen_over(Args A, const int8_t* board
         const int c = SRC == 0 ? A.max_moves : cap;
         int total;
         bool ovf;
-        int nm;
-        if (TIER == 1)
-            nm = run_movegen<kLogMid>(bv, pl, r0, r1, out, c, lds_tab, cap_fast<kLogMid>(), &total, &ovf, memo);
-        else
-            nm = run_movegen<kLogSlotsSlow>(bv, pl, r0, r1, out, c, tab, kCapSlow, &total, &ovf, memo);
+        int nm = run_movegen<kLogMid>(bv, pl, r0, r1, out, c, lds_tab, A.cap_mid, &total, &ovf, memo);
+        if (ovf) nm = run_movegen<kLogSlotsSlow>(bv, pl, r0, r1, out, c, slow, kCapSlow, &total, &ovf, memo);
         if (ovf) {
-            if (TIER == 1) {
-                if (l == 0) { const int q2 = atomicAdd(A.ovf_count + 1, 1); A.ovf_queue[A.B + q2] = gi; }
-                continue;
-            }
             if (l == 0) atomicOr(A.err, 1);
             nm = 0; total = 0;
         }
@@ -553,21 +549,14 @@ static int heavy_grid(int B, bool xcd) {
     return h > B ? B : h;
 }
 
-constexpr int kTier1Grid = 256;      // workgroups of the step's first overflow tier
-
 static int slow_path(bgx_engine* e, hipStream_t s, int src, const int8_t* boards, const uint8_t* players,
                      const uint8_t* dice, int cap, int16_t* nm, int32_t* nt, uint64_t* moves) {
-    if (src == 0) {
-        hipLaunchKernelGGL((k_movegen_over<0, 1>), dim3(kTier1Grid), dim3(64), 0, s, e->a, boards, players, dice,
-                           cap, nm, nt, moves, e->slow_tables);
-        hipLaunchKernelGGL((k_movegen_over<0, 2>), dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice,
-                           cap, nm, nt, moves, e->slow_tables);
-    } else {
-        hipLaunchKernelGGL((k_movegen_over<1, 1>), dim3(256), dim3(64), 0, s, e->a, boards, players, dice, cap, nm, nt,
-                           moves, e->slow_tables);
-        hipLaunchKernelGGL((k_movegen_over<1, 2>), dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice,
-                           cap, nm, nt, moves, e->slow_tables);
-    }
+    if (src == 0)
+        hipLaunchKernelGGL(k_movegen_over<0>, dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice, cap,
+                           nm, nt, moves, e->slow_tables);
+    else
+        hipLaunchKernelGGL(k_movegen_over<1>, dim3(e->slow_waves), dim3(64), 0, s, e->a, boards, players, dice, cap,
+                           nm, nt, moves, e->slow_tables);
     CKL();
     return BGX_OK;
 }
@@ -591,6 +580,11 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     A.key0 = (uint32_t)seed; A.key1 = (uint32_t)(seed >> 32);
     A.xcd = batch % 128 == 0 && bgx_dbg_int("BGX_XCD", 1) != 0 ? 1 : 0;
     e->step_debug = !bgx_dbg("BGX_STEP_DEBUG").empty();
+    // the overflow tiers' caps (tests force positions through tier 1 and tier 2 with small ones)
+    A.cap_mid = (int)std::min<long long>(std::max<long long>(bgx_dbg_int("BGX_TIER1_CAP", cap_fast<kLogMid>()), 1),
+                                         cap_fast<kLogMid>());
+    A.cap_main = (int)std::min<long long>(std::max<long long>(bgx_dbg_int("BGX_MOVEGEN_CAP", cap_fast<9>()), 1),
+                                          cap_fast<9>());
     e->slow_waves = kSlowWaves;
     const size_t B = (size_t)batch;
     hipError_t err = hipSuccess;
@@ -603,7 +597,7 @@ int bgx_engine_create(int device, int32_t batch, int32_t max_moves, uint64_t see
     alloc((void**)&A.shared_rolls, B * 4);
     alloc((void**)&e->ovf_base, 32);
     A.ovf_count = e->ovf_base;
-    alloc((void**)&A.ovf_queue, 2 * B * 4);
+    alloc((void**)&A.ovf_queue, B * 4);
     alloc((void**)&A.err, 16);
     alloc((void**)&e->slow_tables, (size_t)kSlowWaves * ((size_t)16 << kLogSlotsSlow));
     if (!bgx_dbg("BGX_STAMPS").empty()) alloc((void**)&A.stamps, B * 16);
@@ -850,7 +844,7 @@ int bgx_step(bgx_engine* e, const int32_t* actions_dev, float* obs_dev, float* r
         int32_t q[2] = {0, 0};
         CK(hipMemcpyAsync(q, A.ovf_count, 8, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
-        fprintf(stderr, "[bgx step] tier1 %d tier2 %d of %d lanes\n", q[0], q[1], A.B);
+        fprintf(stderr, "[bgx step] overflow queue %d of %d lanes\n", q[0], A.B);
         for (int i = 0; i < q[0] && i < 4; ++i) {
             int32_t gi = 0;
             uint8_t rec[64];
@@ -882,7 +876,7 @@ int bgx_movegen(bgx_engine* e, const int8_t* boards52_dev, const uint8_t* player
     CK(use.err);
     CK(hipMemsetAsync(e->a.ovf_count, 0, 16, s));
     LAUNCH_LOG(e, k_movegen, dim3(n), s, boards52_dev, players_dev, dice_dev, n, max_moves, n_moves_dev, n_total_dev,
-               moves_dev, e->a.ovf_count, e->a.ovf_queue);
+               moves_dev, e->a.ovf_count, e->a.ovf_queue, e->a.cap_main);
     CKL();
     return slow_path(e, s, 1, boards52_dev, players_dev, dice_dev, max_moves, n_moves_dev, n_total_dev, moves_dev);
 }

@@ -38,6 +38,29 @@ def test_movegen_matches_reference(bgx, golden, cap):
     assert eng.error() == 0
 
 
+@pytest.mark.parametrize("caps", [("4", "24"), ("1", "1")])
+def test_movegen_overflow_tiers_vs_reference(bgx, golden, dbg, caps):
+    """Positions through the overflow launch (k_movegen_over): the main table's cap of
+    caps[0] unique afterstates sends almost every golden position to tier 1 (4,096-slot
+    LDS table), whose cap of caps[1] sends most of those on to tier 2 (the workgroup's
+    131,072-slot HBM table, in the same wave since round 6).  The lists equal the
+    reference's golden ones, as without the caps."""
+    dbg.setenv("BGX_MOVEGEN_CAP", caps[0])
+    dbg.setenv("BGX_TIER1_CAP", caps[1])             # read at engine creation
+    g = golden("movegen")
+    n = len(g["counts"])
+    eng = bgx.Engine(batch=n, max_moves=2048, dice="philox")
+    nm, nt, mv = eng.movegen(torch.from_numpy(g["boards"]), torch.from_numpy(g["players"]),
+                             torch.from_numpy(g["rolls"]), max_moves=2048)
+    nm, nt, mv = nm.cpu().numpy(), nt.cpu().numpy(), mv.cpu().numpy().view(np.uint64)
+    ref = _split_golden_moves(g)
+    assert np.array_equal(nt, g["counts"])
+    for i in range(n):
+        k = int(nm[i])
+        assert np.array_equal(mv[i, :k], ref[i][:k]), i
+    assert eng.error() == 0
+
+
 def test_movegen_random_positions_vs_oracle(bgx):
     rng = np.random.RandomState(7)
     n = 6000
