@@ -203,3 +203,44 @@ for _k, _v in {0: 2, 11: 5, 16: 3, 18: 5}.items():
     INITIAL_BOARD52[_k] = _v
 for _k, _v in {23: 2, 12: 5, 7: 3, 5: 5}.items():
     INITIAL_BOARD52[24 + _k] = _v
+
+def leaf_values(W1, b1, w2, b2, keys, tags, side, ml):
+    """V in fp64 of every valid 2-ply leaf-pool slot, from the evaluator's own inputs read
+    back from the device (bgx_debug_option BGX_2PLY_DUMP: the 16-byte keys -- the replier's
+    nibbles, bar, off, hit mask --, the tags, the rows' mover sides and the jobs' final max
+    lengths), encoded as immutable_board.py:171-212 with the root mover's one-hot (DESIGN.md
+    §5) and put through relu(F W1^T + b1) w2 + b2.  Returns (slot indices, V)."""
+    keys = np.asarray(keys); tags = np.asarray(tags); side = np.asarray(side); ml = np.asarray(ml)
+    used = tags != 0xFFFFFFFF
+    job = (tags & 0x1FFFFFFF).astype(np.int64)
+    valid = used & (ml[np.where(used, job, 0)] == (tags >> 29))
+    idx = np.nonzero(valid)[0]
+    k, jb = keys[idx], job[idx]
+    rs = side[jb // 21]
+    q = ((rs[:, 3] >> 8) & 1).astype(np.int64)
+    hits = k[:, 3] >> 8
+
+    def nib(lo, hi):
+        v = np.zeros((len(lo), 24), np.int64)
+        for p in range(16):
+            v[:, p] = (lo >> np.uint64(4 * p)) & np.uint64(15)
+        for p in range(8):
+            v[:, 16 + p] = (hi >> np.uint32(4 * p)) & np.uint32(15)
+        return v
+    qn = nib(k[:, 0].astype(np.uint64) | (k[:, 1].astype(np.uint64) << np.uint64(32)), k[:, 2])
+    hb = np.stack([(hits >> p) & 1 for p in range(24)], 1).astype(np.int64)
+    mn = nib(rs[:, 0].astype(np.uint64) | (rs[:, 1].astype(np.uint64) << np.uint64(32)), rs[:, 2]) - hb
+    bars = [k[:, 3] & 15, (rs[:, 3] & 15) + hb.sum(1)]
+    offs = [(k[:, 3] >> 4) & 15, (rs[:, 3] >> 4) & 15]
+    F = np.zeros((len(idx), 198))
+    for P in range(2):
+        rep = (q == P)[:, None]
+        cnt = np.where(rep, qn, mn)
+        F[:, 98 * P + 0:96 + 98 * P:4] = cnt >= 1
+        F[:, 98 * P + 1:96 + 98 * P:4] = cnt >= 2
+        F[:, 98 * P + 2:96 + 98 * P:4] = cnt >= 3
+        F[:, 98 * P + 3:96 + 98 * P:4] = np.where(cnt >= 3, (cnt - 3) / 2.0, 0)
+        F[:, 96 + 98 * P] = np.where(q == P, bars[0], bars[1]) / 2.0
+        F[:, 97 + 98 * P] = np.where(q == P, offs[0], offs[1]) / 15.0
+    F[np.arange(len(idx)), 196 + (1 - q)] = 1.0        # the root mover's one-hot
+    return idx, np.maximum(F @ np.asarray(W1, np.float64).T + np.asarray(b1, np.float64), 0) @ np.asarray(w2, np.float64) + b2

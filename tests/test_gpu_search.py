@@ -269,46 +269,11 @@ def test_two_ply_full_batch_paths_agree(dbg):
 
 
 def _leaf_reference(net, keys, tags, side, ml):
-    """V of every valid pool leaf in fp64 from its 16-byte key (the replier's nibbles,
-    bar, off, hit mask), its row's mover side and its job's final max length (the
-    evaluator's own inputs, read back from the device): DESIGN.md §5."""
-    used = tags != 0xFFFFFFFF
-    job = (tags & 0x1FFFFFFF).astype(np.int64)
-    valid = used & (ml[np.where(used, job, 0)] == (tags >> 29))
-    idx = np.nonzero(valid)[0]
-    k, jb = keys[idx], job[idx]
-    rs = side[jb // 21]
-    q = ((rs[:, 3] >> 8) & 1).astype(np.int64)
-    hits = k[:, 3] >> 8
-
-    def nib(lo, hi):
-        v = np.zeros((len(lo), 24), np.int64)
-        for p in range(16):
-            v[:, p] = (lo >> np.uint64(4 * p)) & np.uint64(15)
-        for p in range(8):
-            v[:, 16 + p] = (hi >> np.uint32(4 * p)) & np.uint32(15)
-        return v
-    qn = nib(k[:, 0].astype(np.uint64) | (k[:, 1].astype(np.uint64) << np.uint64(32)), k[:, 2])
-    hb = np.stack([(hits >> p) & 1 for p in range(24)], 1).astype(np.int64)
-    mn = nib(rs[:, 0].astype(np.uint64) | (rs[:, 1].astype(np.uint64) << np.uint64(32)), rs[:, 2]) - hb
-    bars = [k[:, 3] & 15, (rs[:, 3] & 15) + hb.sum(1)]
-    offs = [(k[:, 3] >> 4) & 15, (rs[:, 3] >> 4) & 15]
-    F = np.zeros((len(idx), 198))
-    for P in range(2):                           # immutable_board.py:171-212 encoding
-        rep = (q == P)[:, None]
-        cnt = np.where(rep, qn, mn)
-        F[:, 98 * P + 0:96 + 98 * P:4] = cnt >= 1
-        F[:, 98 * P + 1:96 + 98 * P:4] = cnt >= 2
-        F[:, 98 * P + 2:96 + 98 * P:4] = cnt >= 3
-        F[:, 98 * P + 3:96 + 98 * P:4] = np.where(cnt >= 3, (cnt - 3) / 2.0, 0)
-        F[:, 96 + 98 * P] = np.where(q == P, bars[0], bars[1]) / 2.0
-        F[:, 97 + 98 * P] = np.where(q == P, offs[0], offs[1]) / 15.0
-    F[np.arange(len(idx)), 196 + (1 - q)] = 1.0        # the root mover's one-hot
-    W1 = net.fc1.weight.detach().cpu().double().numpy()
-    b1 = net.fc1.bias.detach().cpu().double().numpy()
-    w2 = net.value_head.weight.detach().cpu().double().numpy().ravel()
-    b2 = float(net.value_head.bias.detach().cpu())
-    return idx, np.maximum(F @ W1.T + b1, 0) @ w2 + b2
+    """V of every valid pool leaf in fp64 (oracle.leaf_values)."""
+    import oracle as O
+    return O.leaf_values(net.fc1.weight.detach().cpu().double().numpy(), net.fc1.bias.detach().cpu().double().numpy(),
+                         net.value_head.weight.detach().cpu().double().numpy().ravel(),
+                         float(net.value_head.bias.detach().cpu()), keys, tags, side, ml)
 
 
 @pytest.mark.parametrize("unfactored", [False, True])
