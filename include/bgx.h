@@ -445,6 +445,15 @@ int bgx_gather_rollout(const int32_t* perm_dev, int32_t n, const uint8_t* record
                        const float* old_logp_dev, const float* returns_dev, const float* adv_dev,
                        uint8_t* records_out, int32_t* actions_out, float* old_logp_out, float* returns_out,
                        float* adv_out, void* stream);
+/* bgx_ppo_plan and bgx_gather_rollout in one pass (round 6): the plan, and each row's
+ * record and four fields written straight to its plan-order position (the scatter reads
+ * the records once, coalesced; no perm pass, no random-read gather).  perm_or_null: the
+ * permutation too (tests).  Same workspace; records and records_out 16-byte aligned. */
+int bgx_ppo_plan_rows(const uint8_t* records_dev, int32_t m, int32_t n_actions, int32_t* workspace_dev,
+                      const int32_t* actions_dev, const float* old_logp_dev, const float* returns_dev,
+                      const float* adv_dev, uint8_t* records_out, int32_t* actions_out, float* old_logp_out,
+                      float* returns_out, float* adv_out, int32_t* perm_or_null, int32_t* plan_dev,
+                      int32_t* row_plan_dev, void* stream);
 
 /* Phase times of the last bgx_two_ply call on e (first round, HIP events on the
  * caller's stream): ms2[0] = reply enumeration (all tiers), ms2[1] = leaf

@@ -86,6 +86,7 @@ SIGNATURES = {
     "bgx_gather_rollout": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "bgx_ppo_plan_workspace": (ctypes.c_int64, [_I32]),
     "bgx_ppo_plan": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P]),
+    "bgx_ppo_plan_rows": (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "bgx_debug_option": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
     "bgx_last_error": (ctypes.c_char_p, []),
     "bgx_build_id": (ctypes.c_char_p, []),

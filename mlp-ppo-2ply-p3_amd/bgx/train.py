@@ -444,6 +444,35 @@ def gather_rollout(perm, recs, acts, old, R, adv, out=None):
     return out
 
 
+def plan_rollout(recs, acts, old, R, adv, n_actions: int = 500, out_rows=None, out_plan=None):
+    """ppo_row_plan + gather_rollout in one pass on the GPU (bgx_ppo_plan_rows: the rows
+    written straight to their plan-order positions).  Returns ((records, actions,
+    old_logp, returns, adv) in plan order, plan, row_plan); out_rows / out_plan (the
+    graphed update's persistent buffers; out_plan = (perm, plan, row_plan), perm unused)
+    to write into."""
+    if not recs.is_cuda:
+        perm, plan, row_plan = ppo_row_plan_torch(recs, n_actions)
+        return gather_rollout(perm, recs, acts, old, R, adv), plan, row_plan
+    acts, old, R, adv = (acts.to(torch.int32).contiguous(), old.float().contiguous(), R.float().contiguous(),
+                         adv.float().contiguous())
+    rec = recs.contiguous()
+    m, dev = rec.shape[0], rec.device
+    L = _lib.load()
+    ws = torch.empty(max(int(L.bgx_ppo_plan_workspace(m)) // 4, 1), dtype=torch.int32, device=dev)
+    rows = out_rows if out_rows is not None else (torch.empty_like(rec), torch.empty_like(acts), torch.empty_like(old),
+                                                  torch.empty_like(R), torch.empty_like(adv))
+    if out_plan is not None:
+        _, plan, row_plan = out_plan
+    else:
+        plan = torch.empty(33, dtype=torch.int32, device=dev)
+        row_plan = torch.empty(8, dtype=torch.int32, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    check(L.bgx_ppo_plan_rows(p(rec), m, n_actions, p(ws), p(acts), p(old), p(R), p(adv), *[p(t) for t in rows], None,
+                              p(plan), p(row_plan), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+          "bgx_ppo_plan_rows")
+    return rows, plan, row_plan
+
+
 def _fused_head_ok(net) -> bool:
     """The fused output layer + loss head (csrc/bg_ppo_fused.hip) is built for the
     reference's shape (H = 128, 500 actions); other shapes take the manual epoch
@@ -1018,8 +1047,8 @@ class PPOTrainer:
             # of the 4 epochs reads them contiguously
             for i, s in enumerate(range(0, N, self.chunk)):
                 e = min(N, s + self.chunk)
-                perm, plan, row_plan = ppo_row_plan(recs[s:e], self.A)
-                sorted_rows[i] = gather_rollout(perm, recs[s:e], acts[s:e], old[s:e], R[s:e], adv[s:e])
+                sorted_rows[i], plan, row_plan = plan_rollout(recs[s:e], acts[s:e], old[s:e], R[s:e], adv[s:e],
+                                                              self.A)
                 preps[i] = {"plan": (None, plan, row_plan)}
 
         def chunks():
@@ -1064,8 +1093,8 @@ class PPOTrainer:
                              torch.empty(8, dtype=torch.int32, **kw))})
             self._ugraph = None
         for (s, e), c in zip(spans, self._ubufs["chunks"]):
-            perm, _, _ = ppo_row_plan(recs[s:e], self.A, out=c["plan"])
-            gather_rollout(perm, recs[s:e], acts[s:e], old[s:e], R[s:e], adv[s:e], out=c["rows"])
+            plan_rollout(recs[s:e], acts[s:e], old[s:e], R[s:e], adv[s:e], self.A, out_rows=c["rows"],
+                         out_plan=c["plan"])
 
         def chunks():
             for c in self._ubufs["chunks"]:

@@ -993,15 +993,12 @@ __device__ __forceinline__ int plan_class(const uint8_t* rec, int64_t i, int n_a
     return (lim + 31) >> 5;
 }
 
-// per-wave class counts of this block's rows (LDS wc[16][17]); returns the row's class
-// (0 past the end) and its rank among the wave's rows of that class
-__device__ __forceinline__ int plan_wave_counts(const uint8_t* rec, int m, int n_actions, int (*wc)[kPlanCls],
-                                                int& rank) {
-    const int64_t i = (int64_t)blockIdx.x * kPlanRows + threadIdx.x;
-    const int c = i < m ? plan_class(rec, i, n_actions) : 0;
+// per-wave class counts of this block's rows (LDS wc[16][17]) for the row's class c (0
+// past the end); returns its rank among the wave's rows of that class
+__device__ __forceinline__ int plan_wave_counts(int c, int (*wc)[kPlanCls]) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     const uint64_t below = (1ull << l) - 1ull;
-    rank = 0;
+    int rank = 0;
     #pragma unroll
     for (int k = 1; k < kPlanCls; ++k) {
         const uint64_t b = __ballot(c == k);
@@ -1010,42 +1007,56 @@ __device__ __forceinline__ int plan_wave_counts(const uint8_t* rec, int m, int n
     }
     if (l == 0) wc[w][0] = 0;
     __syncthreads();
-    return c;
+    return rank;
 }
 
+// bcnt class-major: bcnt[k][b] = block b's class-k rows
 __global__ __launch_bounds__(kPlanRows) void k_plan_count(const uint8_t* __restrict__ rec, int m, int n_actions,
                                                           int32_t* __restrict__ bcnt) {
     __shared__ int wc[kPlanRows / 64][kPlanCls];
-    int rank;
-    (void)plan_wave_counts(rec, m, n_actions, wc, rank);
+    const int64_t i = (int64_t)blockIdx.x * kPlanRows + threadIdx.x;
+    (void)plan_wave_counts(i < m ? plan_class(rec, i, n_actions) : 0, wc);
     if (threadIdx.x < kPlanCls) {
         int t = 0;
         #pragma unroll
         for (int w = 0; w < kPlanRows / 64; ++w) t += wc[w][threadIdx.x];
-        bcnt[(size_t)blockIdx.x * kPlanCls + threadIdx.x] = t;
+        bcnt[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = t;
     }
 }
 
-// one workgroup, wave k - 1 scanning class k over the blocks: boff[b][k] = the sorted
-// position of block b's first class-k row; then the plan from the class totals
+// one workgroup, wave k - 1 scanning class k over the blocks: boff[k][b] = the position of
+// block b's first class-k row among the class-k rows, base[k] = the class's first sorted
+// position; then the plan from the class totals.  Round 6: the counts class-major, each
+// lane's 32 loads in flight before the scans (was one strided load per 64 blocks in a
+// dependent chain: 52 us per 2^21 rows)
+constexpr int kPlanScanRegs = 32;
 __global__ __launch_bounds__(1024) void k_plan_scan(const int32_t* __restrict__ bcnt, int nb, int m,
-                                                    int32_t* __restrict__ boff, int32_t* __restrict__ plan,
-                                                    int32_t* __restrict__ row_plan) {
+                                                    int32_t* __restrict__ boff, int32_t* __restrict__ gbase,
+                                                    int32_t* __restrict__ plan, int32_t* __restrict__ row_plan) {
     __shared__ int tot[kPlanCls];
-    __shared__ int base[kPlanCls];
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63, k = w + 1;
+    const int32_t* src = bcnt + (size_t)k * nb;
+    int32_t* dst = boff + (size_t)k * nb;
     int run = 0;
-    for (int b0 = 0; b0 < nb; b0 += 64) {
-        const int b = b0 + l;
-        const int v = b < nb ? bcnt[(size_t)b * kPlanCls + k] : 0;
-        int x = v;                                       // inclusive scan over the 64 lanes
+    for (int b0 = 0; b0 < nb; b0 += 64 * kPlanScanRegs) {
+        int v[kPlanScanRegs];
         #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (l >= o) x += y;
+        for (int j = 0; j < kPlanScanRegs; ++j) {
+            const int b = b0 + 64 * j + l;
+            v[j] = b < nb ? src[b] : 0;
         }
-        if (b < nb) boff[(size_t)b * kPlanCls + k] = run + x - v;
-        run += __shfl(x, 63);
+        #pragma unroll
+        for (int j = 0; j < kPlanScanRegs; ++j) {
+            const int b = b0 + 64 * j + l;
+            int x = v[j];                                // inclusive scan over the 64 lanes
+            #pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o);
+                if (l >= o) x += y;
+            }
+            if (b < nb) dst[b] = run + x - v[j];
+            run += __shfl(x, 63);
+        }
     }
     if (l == 0) tot[k] = run;
     if (threadIdx.x == 0) tot[0] = 0;
@@ -1053,7 +1064,7 @@ __global__ __launch_bounds__(1024) void k_plan_scan(const int32_t* __restrict__ 
     if (threadIdx.x == 0) {
         int acc = 0;
         int cum[kPlanCls];
-        for (int c = 0; c < kPlanCls; ++c) { base[c] = acc; acc += tot[c]; cum[c] = acc; }
+        for (int c = 0; c < kPlanCls; ++c) { gbase[c] = acc; acc += tot[c]; cum[c] = acc; }
         // ppo_row_plan (bgx/train.py): start[o] = first row tile reaching action tile o
         // (the value column's tile 15: every row); tasks of kTS row tiles per action tile
         const int ntiles = (m + 31) / 32;
@@ -1071,23 +1082,51 @@ __global__ __launch_bounds__(1024) void k_plan_scan(const int32_t* __restrict__ 
         row_plan[0] = 0; row_plan[1] = e[0]; row_plan[2] = e[0]; row_plan[3] = e[1];
         row_plan[4] = e[1]; row_plan[5] = e[2]; row_plan[6] = e[2]; row_plan[7] = ntiles;
     }
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += 1024)
-        #pragma unroll
-        for (int c = 1; c < kPlanCls; ++c) boff[(size_t)b * kPlanCls + c] += base[c];
 }
 
+// each row's sorted position; writes perm (may be null) and, when rows.rec_o is set, the
+// row itself there (round 6: the gather of the update's rows folded into the scatter --
+// the record read once, coalesced, instead of a perm pass and a random-read gather)
+struct PlanRows {
+    const int32_t* act;
+    const float *old, *ret, *adv;
+    uint4* rec_o;
+    int32_t* act_o;
+    float *old_o, *ret_o, *adv_o;
+};
 __global__ __launch_bounds__(kPlanRows) void k_plan_scatter(const uint8_t* __restrict__ rec, int m, int n_actions,
                                                             const int32_t* __restrict__ boff,
-                                                            int32_t* __restrict__ perm) {
+                                                            const int32_t* __restrict__ gbase,
+                                                            int32_t* __restrict__ perm, PlanRows rows) {
     __shared__ int wc[kPlanRows / 64][kPlanCls];
-    int rank;
-    const int c = plan_wave_counts(rec, m, n_actions, wc, rank);
     const int64_t i = (int64_t)blockIdx.x * kPlanRows + threadIdx.x;
-    if (i >= m) return;
-    int off = boff[(size_t)blockIdx.x * kPlanCls + c] + rank;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += wc[w][c];
-    perm[off] = (int32_t)i;
+    const int c = i < m ? plan_class(rec, i, n_actions) : 0;
+    const int rank = plan_wave_counts(c, wc);
+    int off = 0;
+    if (i < m) {
+        off = gbase[c] + boff[(size_t)c * gridDim.x + blockIdx.x] + rank;
+        for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) off += wc[w][c];
+        if (perm) perm[off] = (int32_t)i;
+    }
+    if (rows.rec_o) {
+        // the wave's 64 records, 4 lanes per record (16 bytes each), 16 records per pass: each
+        // store instruction writes whole 64-byte records (a thread per record wrote 16-byte
+        // pieces of 64 different records per instruction: 111 us per 2^21 rows)
+        const int l = threadIdx.x & 63;
+        const int64_t wbase = i - l;
+        #pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int rr = 16 * it + (l >> 2);
+            const int dst = __shfl(off, rr);
+            if (wbase + rr < m) rows.rec_o[(int64_t)dst * 4 + (l & 3)] = ((const uint4*)rec)[(wbase + rr) * 4 + (l & 3)];
+        }
+        if (i < m) {
+            rows.act_o[off] = rows.act[i];
+            rows.old_o[off] = rows.old[i];
+            rows.ret_o[off] = rows.ret[i];
+            rows.adv_o[off] = rows.adv[i];
+        }
+    }
 }
 
 // ---- the optimizer step (bgx_adam_step): torch.optim.Adam(fused=True) driven by
@@ -1328,7 +1367,23 @@ extern "C" int bgx_gather_rollout(const int32_t* perm, int32_t n, const uint8_t*
 extern "C" int64_t bgx_ppo_plan_workspace(int32_t m) {
     if (m < 0) return BGX_EINVAL;
     const int64_t nb = ((int64_t)m + kPlanRows - 1) / kPlanRows;
-    return 2 * nb * kPlanCls * 4;
+    return (2 * nb * kPlanCls + kPlanCls) * 4;
+}
+
+static int ppo_plan(const uint8_t* records, int32_t m, int32_t n_actions, int32_t* workspace, int32_t* perm,
+                    const PlanRows& rows, int32_t* plan, int32_t* row_plan, void* stream) {
+    const int nb = (m + kPlanRows - 1) / kPlanRows;
+    hipStream_t s = (hipStream_t)stream;
+    int32_t* bcnt = workspace;
+    int32_t* boff = workspace + (size_t)nb * kPlanCls;
+    int32_t* gbase = boff + (size_t)nb * kPlanCls;
+    if (nb > 0) hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, bcnt);
+    hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, bcnt, nb, m, boff, gbase, plan, row_plan);
+    if (nb > 0)
+        hipLaunchKernelGGL(k_plan_scatter, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, boff, gbase, perm,
+                           rows);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
 }
 
 extern "C" int bgx_ppo_plan(const uint8_t* records, int32_t m, int32_t n_actions, int32_t* workspace, int32_t* perm,
@@ -1336,15 +1391,22 @@ extern "C" int bgx_ppo_plan(const uint8_t* records, int32_t m, int32_t n_actions
     if (m < 0 || n_actions <= 0 || n_actions > kNT * 32 - 1 || (m > 0 && (!records || !workspace || !perm)) ||
         !plan || !row_plan)
         return BGX_EINVAL;
-    const int nb = (m + kPlanRows - 1) / kPlanRows;
-    hipStream_t s = (hipStream_t)stream;
-    int32_t* bcnt = workspace;
-    int32_t* boff = workspace + (size_t)nb * kPlanCls;
-    if (nb > 0) hipLaunchKernelGGL(k_plan_count, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, bcnt);
-    hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, s, bcnt, nb, m, boff, plan, row_plan);
-    if (nb > 0) hipLaunchKernelGGL(k_plan_scatter, dim3(nb), dim3(kPlanRows), 0, s, records, m, n_actions, boff, perm);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? BGX_OK : bgx_internal_fail(e);
+    return ppo_plan(records, m, n_actions, workspace, perm, PlanRows{}, plan, row_plan, stream);
+}
+
+extern "C" int bgx_ppo_plan_rows(const uint8_t* records, int32_t m, int32_t n_actions, int32_t* workspace,
+                                 const int32_t* actions, const float* old_logp, const float* returns, const float* adv,
+                                 uint8_t* records_out, int32_t* actions_out, float* old_logp_out, float* returns_out,
+                                 float* adv_out, int32_t* perm_or_null, int32_t* plan, int32_t* row_plan,
+                                 void* stream) {
+    if (m < 0 || n_actions <= 0 || n_actions > kNT * 32 - 1 || !plan || !row_plan ||
+        (m > 0 && (!records || !workspace || !actions || !old_logp || !returns || !adv || !records_out ||
+                   !actions_out || !old_logp_out || !returns_out || !adv_out)))
+        return BGX_EINVAL;
+    if (((uintptr_t)records | (uintptr_t)records_out) % 16) return BGX_EINVAL;
+    const PlanRows rows{actions, old_logp, returns, adv, (uint4*)records_out, actions_out, old_logp_out, returns_out,
+                        adv_out};
+    return ppo_plan(records, m, n_actions, workspace, perm_or_null, rows, plan, row_plan, stream);
 }
 
 // The fused epoch's gradients into the parameters' .grad tensors, scaled by `post` in

@@ -434,6 +434,32 @@ def test_gather_rollout_matches_torch_indexing():
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("m", [1, 1000, 4097, 3 * 65536 + 77, (1 << 21) + 3])
+def test_plan_rows_matches_plan_then_gather(m):
+    """bgx_ppo_plan_rows (the rows scattered straight to their plan-order positions) ==
+    bgx_ppo_plan + bgx_gather_rollout == the torch plan + torch indexing, bit for bit:
+    legal counts 0 (every action) .. 600 (clamped to 500), a ragged last block, and more
+    than 64 x 32 counting blocks (the scan's register chunks wrap)."""
+    from bgx.train import gather_rollout, plan_rollout, ppo_row_plan, ppo_row_plan_torch
+    g = torch.Generator(device="cuda").manual_seed(5)
+    recs = torch.randint(0, 256, (m, 64), dtype=torch.uint8, device="cuda", generator=g)
+    cnt = torch.randint(0, 601, (m,), device="cuda", generator=g)
+    cnt = torch.where(torch.rand(m, device="cuda", generator=g) < 0.7, cnt % 40, cnt)   # mostly class 1-2
+    recs[:, 60] = (cnt & 255).to(torch.uint8)
+    recs[:, 61] = (cnt >> 8).to(torch.uint8)
+    acts = torch.randint(0, 500, (m,), dtype=torch.int32, device="cuda", generator=g)
+    old, R, adv = (torch.randn(m, device="cuda", generator=g) for _ in range(3))
+    rows, plan, row_plan = plan_rollout(recs, acts, old, R, adv)
+    perm, plan2, row_plan2 = ppo_row_plan(recs)
+    ref = gather_rollout(perm, recs, acts, old, R, adv)
+    permt, plant, row_plant = ppo_row_plan_torch(recs)
+    assert torch.equal(perm, permt)
+    assert torch.equal(plan, plan2) and torch.equal(plan, plant)
+    assert torch.equal(row_plan, row_plan2) and torch.equal(row_plan, row_plant)
+    for a, b in zip(rows, ref):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("m", [1, 31, 1024, 4097, 3 * 65536 + 77, (1 << 20) + 5])
 def test_device_row_plan_matches_torch(m):
     """bgx_ppo_plan (stable counting sort by action-tile class + the k_ppo_gw2 / rows
