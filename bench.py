@@ -919,12 +919,13 @@ def main():
         line["two_ply_h128"] = two_ply_bench([eng2], 1, ws, dev, hidden=128)
         enums = (summ or {}).get("two_ply_enum") if prof_ok else None
         if enums:
-            # tools/profile.sh's enum passes run --two-ply-batches 1: a warm and a timed batch
-            # at H = 40 (as shards), then at H = 128 -- 4 enumerations of the B roots; priced
-            # over the whole-batch enumeration window of the one-engine H = 128 leg (the
-            # enumeration does not depend on H)
+            # tools/profile.sh's enum passes run --two-ply-batches 1 with the default 4 shards:
+            # a warm and a timed batch in each of the three legs (H = 40 as shards and as one
+            # engine, H = 128 as one engine) -- 6 enumerations of the B roots (round 5 divided
+            # by 4); priced over the whole-batch enumeration window of the one-engine H = 128
+            # leg (the enumeration does not depend on H)
             line["two_ply"]["roofline_issue"] = enum_roofline(
-                enums, 4, line["two_ply_h128"]["enumeration_ms_per_batch"],
+                enums, 6, line["two_ply_h128"]["enumeration_ms_per_batch"],
                 summ.get("enum_command", "python bench.py " + EVAL_PMC_ARGS))
         if eng2 is not engs[0]:             # its 2-ply leaf pool and workspaces (~11 GB) go back
             del eng2
