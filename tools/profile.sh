@@ -9,6 +9,7 @@
 #                  env step's issue-rate roofline)
 #   mfma / efetch  the 2-ply evaluators (H 40 and H 128): MFMA busy cycles + VALU
 #                  counters, and HBM read bytes
+#   eval2          the evaluators' wave-time split
 #   pol1 / pol2    the C3 policy kernel k_policy_act: MFMA / VALU issue, wave-time split
 #   enum1 / enum2  the 2-ply reply enumerators: instruction mix, wave-time split
 # Summary -> gpurun_out/$TAG/summary.json.   Usage: tools/profile.sh TAG [bench args...]
@@ -30,6 +31,8 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_IN
 EVAL_ARGS="--steps 2 --warmup 1 --burn-in 150 --horizon 0 --no-cpu-baseline --two-ply-batches 1 --c2-steps 0 --mirror-steps 0"
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_MFMA SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU --kernel-include-regex "k_eval" --output-format csv -d $OUT/mfma -o run -- python bench.py $EVAL_ARGS > $OUT/mfma.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_eval" --output-format csv -d $OUT/efetch -o run -- python bench.py $EVAL_ARGS > $OUT/efetch.log 2>&1
+# the evaluators' wave-time split (round 6)
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU --kernel-include-regex "k_eval" --output-format csv -d $OUT/eval2 -o run -- python bench.py $EVAL_ARGS > $OUT/eval2.log 2>&1
 # the C3 policy kernel (k_policy_act, round 4): MFMA / VALU issue and the wave-time split
 POL='k_policy_act'
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES --kernel-include-regex "$POL" --output-format csv -d $OUT/pol1 -o run -- python bench.py $PMC_ARGS > $OUT/pol1.log 2>&1

@@ -181,6 +181,16 @@ if sq:
 # 32 per v_mfma_f32_32x32x16; MI355X_MICROARCH.md constants table) over 1,024 SIMDs x
 # its duration at 2.4 GHz; VALU instructions / active quad-cycles; HBM read bytes
 # (2 x FETCH_SIZE KiB, the guide's 16-B streaming correction)
+def wave_split(m):
+    wc = statistics.mean(m["SQ_WAVE_CYCLES"]) if "SQ_WAVE_CYCLES" in m else 0
+    if not wc:
+        return None
+    f = lambda c: statistics.mean(m[c]) / wc if c in m else None
+    return {"active_any": f("SQ_ACTIVE_INST_ANY"), "wait_any (s_waitcnt / barrier)": f("SQ_WAIT_ANY"),
+            "wait_inst_any (issue stall)": f("SQ_WAIT_INST_ANY"), "wait_inst_lds": f("SQ_WAIT_INST_LDS"),
+            "active_lds": f("SQ_ACTIVE_INST_LDS"), "active_valu": f("SQ_ACTIVE_INST_VALU")}
+
+
 mrows, erows = pmc_rows("mfma"), pmc_rows("efetch")
 evals = []
 for k in kernels:
@@ -203,6 +213,9 @@ for k in kernels:
     f = erows.get(k["name"], {}).get("FETCH_SIZE")
     if f:
         e["hbm_read_bytes"] = 2 * statistics.mean(f) * 1024
+    w2 = pmc_rows("eval2").get(k["name"], {})      # round 6: the evaluator's wave-time split
+    if w2:
+        e["wave_time_split"] = wave_split(w2)
     evals.append(e)
 
 # ------------------------------------------------- C3 policy kernel (round 4) --
@@ -220,16 +233,6 @@ def merged(kinds, pred):
                 for c, vals in v.items():
                     d.setdefault(c, vals)
     return res
-
-
-def wave_split(m):
-    wc = statistics.mean(m["SQ_WAVE_CYCLES"]) if "SQ_WAVE_CYCLES" in m else 0
-    if not wc:
-        return None
-    f = lambda c: statistics.mean(m[c]) / wc if c in m else None
-    return {"active_any": f("SQ_ACTIVE_INST_ANY"), "wait_any (s_waitcnt / barrier)": f("SQ_WAIT_ANY"),
-            "wait_inst_any (issue stall)": f("SQ_WAIT_INST_ANY"), "wait_inst_lds": f("SQ_WAIT_INST_LDS"),
-            "active_lds": f("SQ_ACTIVE_INST_LDS"), "active_valu": f("SQ_ACTIVE_INST_VALU")}
 
 
 policy = []
@@ -265,7 +268,7 @@ for name, m in merged(("enum1", "enum2"), lambda n: n.startswith("k_enum")).item
 # figures above can be recomputed from what is committed under profiles/)
 with open(os.path.join(out, "pmc_totals.csv"), "w") as fo:
     fo.write("pass,kernel,counter,dispatches,total\n")
-    for kind in ("fetch", "write", "sqi", "sqc", "mfma", "efetch", "pol1", "pol2", "enum1", "enum2"):
+    for kind in ("fetch", "write", "sqi", "sqc", "mfma", "efetch", "eval2", "pol1", "pol2", "enum1", "enum2"):
         for n, v in pmc_rows(kind).items():
             for c, vals in v.items():
                 fo.write(f"{kind},{short(n).replace(',', ';')},{c},{len(vals)},{sum(vals):.17g}\n")
